@@ -1,0 +1,60 @@
+"""Per-dataset option dictionaries, verbatim from the reference driver.
+
+The keys and values are exactly those of /root/reference/main.py:20-44 (KITTI, ds=0),
+:50-74 (Malaga, ds=1) and :80-104 (Parking, ds=2); ``criteria`` uses the numeric value
+of cv2.TERM_CRITERIA_EPS | cv2.TERM_CRITERIA_COUNT (= 3, main.py:38).  Bootstrap frame
+pairs and sequence lengths are from main.py:17-18, :47-48, :77-78.
+"""
+from __future__ import annotations
+
+import copy
+
+TERM_CRITERIA_COUNT = 1
+TERM_CRITERIA_EPS = 2
+
+_KITTI = {
+    'min_dist_landmarks': 1,
+    'max_dist_landmarks': 150,
+    'min_baseline_angle': 2,
+    'min_baseline_frames': 2,
+    'feature_ratio': 0.8,
+    'feature_max_corners': 1400,
+    'feature_quality_level': 0.1,
+    'feature_min_dist': 10,
+    'feature_block_size': 3,
+    'feature_use_harris': False,
+    'winSize': (15, 15),
+    'maxLevel': 5,
+    'criteria': (TERM_CRITERIA_EPS | TERM_CRITERIA_COUNT, 50, 0.01),
+    'PnP_conf': 0.99,
+    'PnP_error': 8,
+    'PnP_iterations': 500,
+}
+
+_MALAGA = dict(_KITTI, min_dist_landmarks=0, max_dist_landmarks=100, feature_quality_level=0.03,
+               maxLevel=10, PnP_error=5)
+
+_PARKING = dict(_KITTI, max_dist_landmarks=50, maxLevel=10,
+                criteria=(TERM_CRITERIA_EPS | TERM_CRITERIA_COUNT, 50, 0.02), PnP_error=5)
+
+PRESETS = {
+    # name: (options, bootstrap_frames, last_frame)
+    'kitti': (_KITTI, (0, 2), 2761),
+    'malaga': (_MALAGA, (0, 6), 2120),
+    'parking': (_PARKING, (0, 6), 598),
+}
+
+# synthetic-sequence preset -> reference option preset
+SEQ_TO_OPTIONS = {
+    'kitti': 'kitti',
+    'parking': 'parking',
+    'malaga': 'malaga',
+    'malaga1024': 'malaga',
+    'hd1080': 'kitti',
+}
+
+
+def get(name: str):
+    """Return (options dict copy, bootstrap pair, reference last_frame)."""
+    opts, boot, last = PRESETS[SEQ_TO_OPTIONS.get(name, name)]
+    return copy.deepcopy(opts), tuple(boot), last

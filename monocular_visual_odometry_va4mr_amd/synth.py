@@ -1,0 +1,222 @@
+"""Seeded synthetic monocular sequences with ground truth.
+
+The reference reads KITTI / Malaga / Parking frames from disk (``utils.py:55-85``);
+none of those datasets exist here, so every test and benchmark runs on procedurally
+rendered sequences that have the reference's image sizes and intrinsics:
+
+* KITTI 1241x376, K from ``utils.py:22-24``
+* Parking 640x480, K from ``utils.py:43-45``
+* Malaga 800x600 (K ``utils.py:34-36``) and 1024x768 (same K scaled by 1.28)
+* 1920x1080 (KITTI focal scaled to the width)
+
+Scene: a textured "canyon" -- ground plane, two side walls and a ceiling -- whose
+texture is multi-octave value noise, band-limited per pixel by the world-space
+footprint so that far surfaces fade to the mean instead of aliasing.  The camera
+moves forward one unit per frame and yaws sinusoidally (bounded lateral drift).
+Rendering is plain torch in float64 using only elementwise IEEE operations (no BLAS,
+no library RNG), so a frame is bit-identical whether rendered on the CPU or the GPU
+and on any host; this module is data plumbing, not part of the VO hot path.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+K_KITTI = np.array([[7.188560000000e+02, 0, 6.071928000000e+02],
+                    [0, 7.188560000000e+02, 1.852157000000e+02],
+                    [0, 0, 1]])                                   # utils.py:22-24
+K_MALAGA = np.array([[621.18428, 0, 404.0076],
+                     [0, 621.18428, 309.05989],
+                     [0, 0, 1]])                                  # utils.py:34-36
+K_PARKING = np.array([[331.37, 0, 320],
+                      [0, 369.568, 240],
+                      [0, 0, 1]])                                 # utils.py:43-45
+
+SIZES = {
+    "kitti": (1241, 376),
+    "parking": (640, 480),
+    "malaga": (800, 600),
+    "malaga1024": (1024, 768),
+    "hd1080": (1920, 1080),
+}
+
+
+def intrinsics(name: str) -> np.ndarray:
+    if name == "kitti":
+        return K_KITTI.copy()
+    if name == "parking":
+        return K_PARKING.copy()
+    if name == "malaga":
+        return K_MALAGA.copy()
+    if name == "malaga1024":
+        K = K_MALAGA.copy()
+        K[:2] *= 1.28
+        return K
+    if name == "hd1080":
+        K = K_KITTI.copy()
+        s = 1920.0 / 1241.0
+        K[0, 0] *= s
+        K[1, 1] *= s
+        K[0, 2] = 959.5
+        K[1, 2] = 539.5
+        return K
+    raise ValueError(f"unknown sequence preset {name!r}")
+
+
+@dataclass
+class SceneParams:
+    cam_height: float = 1.65      # ground plane at y = +cam_height (y down)
+    ceiling: float = 7.0          # ceiling plane at y = -ceiling
+    wall: float = 9.0             # side walls at x = +-wall
+    speed: float = 1.0            # units per frame along the heading
+    yaw_amp_deg: float = 5.0      # heading amplitude
+    yaw_period: float = 300.0     # frames per heading period
+    mean: float = 110.0
+    contrast: float = 90.0
+    noise_sigma: float = 2.0
+    octaves: int = 10
+    base_wavelength: float = 8.0  # world units of the coarsest octave
+    persistence: float = 1.0
+
+
+def poses(n_frames: int, p: SceneParams, start: int = 0):
+    """Ground-truth camera->world rotations and centres for frames [start, start+n)."""
+    Rs, cs = [], []
+    c = np.zeros(3)
+    # integrate from frame 0 so that any window of the sequence is consistent
+    for k in range(start + n_frames):
+        th = math.radians(p.yaw_amp_deg) * math.sin(2.0 * math.pi * k / p.yaw_period)
+        if k >= start:
+            ct, st = math.cos(th), math.sin(th)
+            R_wc = np.array([[ct, 0.0, st], [0.0, 1.0, 0.0], [-st, 0.0, ct]])
+            Rs.append(R_wc)
+            cs.append(c.copy())
+        c = c + p.speed * np.array([math.sin(th), 0.0, math.cos(th)])
+    return np.stack(Rs), np.stack(cs)
+
+
+def _hash2(ix: torch.Tensor, iy: torch.Tensor, seed: int) -> torch.Tensor:
+    """Integer lattice hash -> float in [-1, 1).  int64 arithmetic, identical on CPU/GPU."""
+    h = ix * 374761393 + iy * 668265263 + seed * 2147483647
+    h = (h ^ (h >> 13)) * 1274126177
+    h = h ^ (h >> 16)
+    return ((h & 0xFFFF).to(torch.float64) / 32768.0) - 1.0
+
+
+def _value_noise(u: torch.Tensor, v: torch.Tensor, seed: int, sharp: torch.Tensor) -> torch.Tensor:
+    """Lattice value noise whose cell-to-cell transition is sharpened by ``sharp``
+    (1 = smooth value noise, large = anti-aliased constant tiles with corners)."""
+    iu = torch.floor(u)
+    iv = torch.floor(v)
+    fu = ((u - iu - 0.5) * sharp + 0.5).clamp(0.0, 1.0)
+    fv = ((v - iv - 0.5) * sharp + 0.5).clamp(0.0, 1.0)
+    iu = iu.to(torch.int64)
+    iv = iv.to(torch.int64)
+    su = fu * fu * (3 - 2 * fu)
+    sv = fv * fv * (3 - 2 * fv)
+    n00 = _hash2(iu, iv, seed)
+    n10 = _hash2(iu + 1, iv, seed)
+    n01 = _hash2(iu, iv + 1, seed)
+    n11 = _hash2(iu + 1, iv + 1, seed)
+    a = n00 + (n10 - n00) * su
+    b = n01 + (n11 - n01) * su
+    return a + (b - a) * sv
+
+
+class Renderer:
+    """Renders frames of one seeded sequence on a torch device."""
+
+    def __init__(self, preset: str = "kitti", seed: int = 0, device="cpu",
+                 params: SceneParams | None = None):
+        self.preset = preset
+        self.W, self.H = SIZES[preset]
+        self.K = intrinsics(preset)
+        self.seed = int(seed)
+        self.p = params or SceneParams()
+        self.device = torch.device(device)
+        fx, fy, cx, cy = (float(self.K[0, 0]), float(self.K[1, 1]), float(self.K[0, 2]),
+                          float(self.K[1, 2]))
+        ys, xs = torch.meshgrid(torch.arange(self.H, dtype=torch.float64),
+                                torch.arange(self.W, dtype=torch.float64), indexing="ij")
+        # camera-frame rays with elementwise IEEE ops only (bit-identical on CPU and GPU)
+        self.rx = ((xs - cx) / fx).to(self.device)
+        self.ry = ((ys - cy) / fy).to(self.device)
+        self.inv_f = 1.0 / fx
+        self.pix = (ys * self.W + xs).to(torch.int64).to(self.device)
+
+    def gt_poses(self, n_frames: int, start: int = 0):
+        return poses(n_frames, self.p, start)
+
+    @torch.no_grad()
+    def render(self, frame_idx: int, R_wc: np.ndarray, c_w: np.ndarray) -> torch.Tensor:
+        p = self.p
+        dev = self.device
+        R = [[float(R_wc[i, j]) for j in range(3)] for i in range(3)]
+        rx, ry = self.rx, self.ry
+        dx = rx * R[0][0] + ry * R[0][1] + R[0][2]
+        dy = rx * R[1][0] + ry * R[1][1] + R[1][2]
+        dz = rx * R[2][0] + ry * R[2][1] + R[2][2]
+        cx, cy, cz = float(c_w[0]), float(c_w[1]), float(c_w[2])
+        big = torch.full_like(dx, 1e9)
+        eps = 1e-6
+        # ground y = +h, ceiling y = -c, walls x = +-w
+        t_g = torch.where(dy > eps, (p.cam_height - cy) / dy.clamp(min=eps), big)
+        t_c = torch.where(dy < -eps, (-p.ceiling - cy) / dy.clamp(max=-eps), big)
+        t_r = torch.where(dx > eps, (p.wall - cx) / dx.clamp(min=eps), big)
+        t_l = torch.where(dx < -eps, (-p.wall - cx) / dx.clamp(max=-eps), big)
+        ts = torch.stack([t_g, t_c, t_r, t_l], 0)
+        t, which = ts.min(0)
+        px = cx + t * dx
+        py = cy + t * dy
+        pz = cz + t * dz
+        # texture coordinates per surface
+        u = torch.where(which < 2, px, pz)
+        v = torch.where(which < 2, pz, py)
+        # pixel footprint in world units, grazing-angle aware
+        dnorm = torch.sqrt(dx * dx + dy * dy + dz * dz)
+        cos_inc = torch.where(which < 2, dy.abs(), dx.abs()) / dnorm
+        foot = t * dnorm * self.inv_f / cos_inc.clamp(min=0.03)
+        val = torch.zeros_like(u)
+        amp = 1.0
+        wl = p.base_wavelength
+        norm = 0.0
+        for o in range(p.octaves):
+            att = ((wl / foot - 2.0) / 2.0).clamp(0.0, 1.0)
+            sharp = (wl / foot / 1.5).clamp(1.0, 60.0)
+            n = torch.zeros_like(u)
+            for s in range(4):
+                m = which == s
+                if bool(m.any()):
+                    n[m] = _value_noise(u[m] / wl, v[m] / wl, int(self.seed * 131 + s * 7919 + o * 31),
+                                        sharp[m])
+            val = val + amp * att * n
+            norm += amp
+            amp *= p.persistence
+            wl *= 0.5
+        img = p.mean + p.contrast * 2.0 * val / norm
+        # sensor noise: Irwin-Hall(4) of hashed uniforms, exact integer hashing
+        base = self.pix + (self.seed * 1000003 + frame_idx) * 2654435761
+        acc = torch.zeros_like(img)
+        for k in range(4):
+            acc = acc + (_hash2(base, torch.full_like(base, k), 17) + 1.0) * 0.5
+        noise = (acc - 2.0) * math.sqrt(3.0) * p.noise_sigma
+        img = torch.round(img + noise).clamp(0, 255).to(torch.uint8)
+        return img
+
+    def frames(self, n_frames: int, start: int = 0):
+        Rs, cs = self.gt_poses(n_frames, start)
+        out = []
+        for i in range(n_frames):
+            out.append(self.render(start + i, Rs[i], cs[i]))
+        return out, Rs, cs
+
+
+def make_sequence(preset: str, n_frames: int, seed: int = 0, start: int = 0, device="cpu"):
+    """Return (frames uint8 [n,H,W] numpy, K, R_wc [n,3,3], c_w [n,3])."""
+    r = Renderer(preset, seed, device)
+    fr, Rs, cs = r.frames(n_frames, start)
+    arr = torch.stack(fr).cpu().numpy()
+    return arr, r.K, Rs, cs

@@ -1,0 +1,597 @@
+/*
+ * vo_oracle_sift.c -- CPU ORACLE (test infrastructure only; see vo_oracle.h).
+ *
+ * Restates OpenCV 4.6 SIFT (features2d/src/sift.simd.hpp) with its defaults
+ * (nfeatures 0, 3 octave layers, contrast 0.04, edge 10, sigma 1.6, upsampled first
+ * octave, float descriptors with integer values) and BFMatcher(NORM_L2).knnMatch(k=2)
+ * as called at VisualOdometryPipeLine.py:35-36,226-229.
+ *
+ * Fixed evaluation orders (mirrored by the HIP path): separable Gaussian taps are
+ * summed k = 0..ksize-1 (row pass, then column pass); histograms accumulate in pixel
+ * order; exp uses OpenCV's exp32f table/polynomial; atan uses OpenCV's fastAtan2
+ * polynomial; sin/cos/pow are evaluated in double and rounded to float.
+ */
+#include "vo_oracle.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define N_LAYERS 3
+#define SIFT_IMG_BORDER 5
+#define SIFT_MAX_INTERP_STEPS 5
+#define SIFT_ORI_HIST_BINS 36
+#define SIFT_ORI_SIG_FCTR 1.5f
+#define SIFT_ORI_RADIUS (3 * SIFT_ORI_SIG_FCTR)
+#define SIFT_ORI_PEAK_RATIO 0.8f
+#define SIFT_DESCR_SCL_FCTR 3.f
+#define SIFT_DESCR_MAG_THR 0.2f
+#define SIFT_INT_DESCR_FCTR 512.f
+#define SIFT_D 4
+#define SIFT_N 8
+
+static inline int refl101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) {
+        if (p < 0) p = -p;
+        else p = 2 * len - p - 2;
+    }
+    return p;
+}
+
+/* ------------------------------------------------ OpenCV hal::exp32f restated */
+#define EXPTAB_SCALE 6
+#define EXPTAB_MASK ((1 << EXPTAB_SCALE) - 1)
+#define EXPPOLY_32F_A0 .9670371139572337719125840413672004409288e-2
+static float g_exptab[64];
+static int g_exptab_init = 0;
+
+static void exptab_init(void)
+{
+    if (g_exptab_init) return;
+    for (int i = 0; i < 64; ++i) g_exptab[i] = (float)(pow(2.0, i / 64.0) * EXPPOLY_32F_A0);
+    g_exptab_init = 1;
+}
+
+static inline float exp32f(float x)
+{
+    const float A4 = (float)(1.000000000000002438532970795181890933776 / EXPPOLY_32F_A0);
+    const float A3 = (float)(.6931471805521448196800669615864773144641 / EXPPOLY_32F_A0);
+    const float A2 = (float)(.2402265109513301490103372422686535526573 / EXPPOLY_32F_A0);
+    const float A1 = (float)(.5550339366753125211915322047004666939128e-1 / EXPPOLY_32F_A0);
+    const float prescale = (float)(1.4426950408889634073599246810019 * (1 << EXPTAB_SCALE));
+    const float postscale = (float)(1. / (1 << EXPTAB_SCALE));
+    float x0 = x * prescale;
+    int xi = (int)lrintf(x0);
+    x0 = (x0 - (float)xi) * postscale;
+    int t = (xi >> EXPTAB_SCALE) + 127;
+    t = !(t & ~255) ? t : (t < 0 ? 0 : 255);
+    union { int32_t i; float f; } buf;
+    buf.i = t << 23;
+    return buf.f * g_exptab[xi & EXPTAB_MASK] * ((((x0 + A1) * x0 + A2) * x0 + A3) * x0 + A4);
+}
+
+/* ------------------------------------------------ OpenCV hal::fastAtan2 (degrees) */
+static inline float fast_atan2(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+/* ------------------------------------------------ images */
+typedef struct { int w, h; float* d; } fimg_t;
+
+static fimg_t fimg_new(int w, int h)
+{
+    fimg_t r = {w, h, (float*)malloc(sizeof(float) * (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1))};
+    return r;
+}
+
+static int gauss_ksize(double sigma) { return ((int)lrint(sigma * 4 * 2 + 1)) | 1; }
+
+static void gauss_kernel(int n, double sigma, float* k)
+{
+    double s2 = -0.5 / (sigma * sigma), sum = 0;
+    for (int i = 0; i < n; ++i) {
+        double x = i - (n - 1) * 0.5;
+        k[i] = (float)exp(s2 * x * x);
+        sum += k[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
+}
+
+/* separable Gaussian, BORDER_REFLECT_101, taps summed in order k = 0..n-1 */
+static void gauss_blur(const fimg_t* src, fimg_t* dst, double sigma)
+{
+    int n = gauss_ksize(sigma), r = n / 2;
+    float k[64];
+    gauss_kernel(n, sigma, k);
+    int w = src->w, h = src->h;
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)w * h);
+    for (int y = 0; y < h; ++y) {
+        const float* s = src->d + (size_t)y * w;
+        for (int x = 0; x < w; ++x) {
+            float acc = 0.f;
+            for (int i = 0; i < n; ++i) acc += k[i] * s[refl101(x - r + i, w)];
+            tmp[(size_t)y * w + x] = acc;
+        }
+    }
+    for (int y = 0; y < h; ++y) {
+        for (int x = 0; x < w; ++x) {
+            float acc = 0.f;
+            for (int i = 0; i < n; ++i) acc += k[i] * tmp[(size_t)refl101(y - r + i, h) * w + x];
+            dst->d[(size_t)y * w + x] = acc;
+        }
+    }
+    free(tmp);
+}
+
+/* 2x INTER_LINEAR upsample of an 8-bit image into float (exact quarter weights) */
+static void upsample2x(const uint8_t* img, int w, int h, fimg_t* dst)
+{
+    int dw = 2 * w, dh = 2 * h;
+    float* row = (float*)malloc(sizeof(float) * dw * 2);
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * 0.5 - 0.5);
+        int sy = (int)floorf(fy);
+        fy -= sy;
+        if (sy < 0) { fy = 0; sy = 0; }
+        if (sy >= h - 1) { fy = 0; sy = h - 1; }
+        int sy1 = sy + 1 < h ? sy + 1 : h - 1;
+        for (int rr = 0; rr < 2; ++rr) {
+            const uint8_t* s = img + (size_t)(rr ? sy1 : sy) * w;
+            for (int dx = 0; dx < dw; ++dx) {
+                float fx = (float)((dx + 0.5) * 0.5 - 0.5);
+                int sx = (int)floorf(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx >= w - 1) { fx = 0; sx = w - 1; }
+                int sx1 = sx + 1 < w ? sx + 1 : w - 1;
+                row[rr * dw + dx] = (float)s[sx] * (1.f - fx) + (float)s[sx1] * fx;
+            }
+        }
+        for (int dx = 0; dx < dw; ++dx)
+            dst->d[(size_t)dy * dw + dx] = row[dx] * (1.f - fy) + row[dw + dx] * fy;
+    }
+    free(row);
+}
+
+/* INTER_NEAREST to (w/2, h/2) */
+static void downsample_nn(const fimg_t* src, fimg_t* dst)
+{
+    int dw = src->w / 2, dh = src->h / 2;
+    double ifx = 1. / ((double)dw / src->w), ify = 1. / ((double)dh / src->h);
+    for (int y = 0; y < dh; ++y) {
+        int sy = (int)floor(y * ify);
+        if (sy > src->h - 1) sy = src->h - 1;
+        for (int x = 0; x < dw; ++x) {
+            int sx = (int)floor(x * ifx);
+            if (sx > src->w - 1) sx = src->w - 1;
+            dst->d[(size_t)y * dw + x] = src->d[(size_t)sy * src->w + sx];
+        }
+    }
+}
+
+typedef struct {
+    float x, y, size, angle, response;
+    int octave;
+} kp_t;
+
+#define AT(im, r, c) ((im)->d[(size_t)(r) * (im)->w + (c)])
+
+/* Matx33f::solve(DECOMP_LU) -> LUImpl<float>; returns 0 and X = 0 when singular */
+static void lu3_solve(float A[9], float b[3], float X[3])
+{
+    const float eps = FLT_EPSILON * 10;
+    for (int i = 0; i < 3; ++i) {
+        int k = i;
+        for (int j = i + 1; j < 3; ++j) if (fabsf(A[j * 3 + i]) > fabsf(A[k * 3 + i])) k = j;
+        if (fabsf(A[k * 3 + i]) < eps) { X[0] = X[1] = X[2] = 0; return; }
+        if (k != i) {
+            for (int j = i; j < 3; ++j) { float t = A[i * 3 + j]; A[i * 3 + j] = A[k * 3 + j]; A[k * 3 + j] = t; }
+            float t = b[i]; b[i] = b[k]; b[k] = t;
+        }
+        float d = -1 / A[i * 3 + i];
+        for (int j = i + 1; j < 3; ++j) {
+            float alpha = A[j * 3 + i] * d;
+            for (int kk = i + 1; kk < 3; ++kk) A[j * 3 + kk] += alpha * A[i * 3 + kk];
+            b[j] += alpha * b[i];
+        }
+        A[i * 3 + i] = -d;
+    }
+    for (int i = 2; i >= 0; --i) {
+        float s = b[i];
+        for (int kk = i + 1; kk < 3; ++kk) s -= A[i * 3 + kk] * b[kk];
+        b[i] = s * A[i * 3 + i];
+    }
+    X[0] = b[0]; X[1] = b[1]; X[2] = b[2];
+}
+
+static int adjust_local_extrema(fimg_t* dog, int nOct_unused, kp_t* kpt, int octv, int* layer,
+                                int* r, int* c, float sigma)
+{
+    (void)nOct_unused;
+    const float contrastThreshold = 0.04f, edgeThreshold = 10.f;
+    const float img_scale = 1.f / (255 * 1);
+    const float deriv_scale = img_scale * 0.5f;
+    const float second_deriv_scale = img_scale;
+    const float cross_deriv_scale = img_scale * 0.25f;
+    float xi = 0, xr = 0, xc = 0, contr = 0;
+    int i = 0;
+    for (; i < SIFT_MAX_INTERP_STEPS; ++i) {
+        int idx = octv * (N_LAYERS + 2) + *layer;
+        fimg_t *img = &dog[idx], *prev = &dog[idx - 1], *next = &dog[idx + 1];
+        int rr = *r, cc = *c;
+        float dD[3] = {(AT(img, rr, cc + 1) - AT(img, rr, cc - 1)) * deriv_scale,
+                       (AT(img, rr + 1, cc) - AT(img, rr - 1, cc)) * deriv_scale,
+                       (AT(next, rr, cc) - AT(prev, rr, cc)) * deriv_scale};
+        float v2 = AT(img, rr, cc) * 2;
+        float dxx = (AT(img, rr, cc + 1) + AT(img, rr, cc - 1) - v2) * second_deriv_scale;
+        float dyy = (AT(img, rr + 1, cc) + AT(img, rr - 1, cc) - v2) * second_deriv_scale;
+        float dss = (AT(next, rr, cc) + AT(prev, rr, cc) - v2) * second_deriv_scale;
+        float dxy = (AT(img, rr + 1, cc + 1) - AT(img, rr + 1, cc - 1) - AT(img, rr - 1, cc + 1) +
+                     AT(img, rr - 1, cc - 1)) * cross_deriv_scale;
+        float dxs = (AT(next, rr, cc + 1) - AT(next, rr, cc - 1) - AT(prev, rr, cc + 1) +
+                     AT(prev, rr, cc - 1)) * cross_deriv_scale;
+        float dys = (AT(next, rr + 1, cc) - AT(next, rr - 1, cc) - AT(prev, rr + 1, cc) +
+                     AT(prev, rr - 1, cc)) * cross_deriv_scale;
+        float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+        float X[3];
+        lu3_solve(H, dD, X);
+        xi = -X[2]; xr = -X[1]; xc = -X[0];
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) ||
+            fabsf(xc) > (float)(INT_MAX / 3))
+            return 0;
+        *c += (int)lrintf(xc);
+        *r += (int)lrintf(xr);
+        *layer += (int)lrintf(xi);
+        if (*layer < 1 || *layer > N_LAYERS || *c < SIFT_IMG_BORDER || *c >= img->w - SIFT_IMG_BORDER ||
+            *r < SIFT_IMG_BORDER || *r >= img->h - SIFT_IMG_BORDER)
+            return 0;
+    }
+    if (i >= SIFT_MAX_INTERP_STEPS) return 0;
+    {
+        int idx = octv * (N_LAYERS + 2) + *layer;
+        fimg_t *img = &dog[idx], *prev = &dog[idx - 1], *next = &dog[idx + 1];
+        int rr = *r, cc = *c;
+        float dD[3] = {(AT(img, rr, cc + 1) - AT(img, rr, cc - 1)) * deriv_scale,
+                       (AT(img, rr + 1, cc) - AT(img, rr - 1, cc)) * deriv_scale,
+                       (AT(next, rr, cc) - AT(prev, rr, cc)) * deriv_scale};
+        float t = dD[0] * xc + dD[1] * xr + dD[2] * xi;
+        contr = AT(img, rr, cc) * img_scale + t * 0.5f;
+        if (fabsf(contr) * N_LAYERS < contrastThreshold) return 0;
+        float v2 = AT(img, rr, cc) * 2.f;
+        float dxx = (AT(img, rr, cc + 1) + AT(img, rr, cc - 1) - v2) * second_deriv_scale;
+        float dyy = (AT(img, rr + 1, cc) + AT(img, rr - 1, cc) - v2) * second_deriv_scale;
+        float dxy = (AT(img, rr + 1, cc + 1) - AT(img, rr + 1, cc - 1) - AT(img, rr - 1, cc + 1) +
+                     AT(img, rr - 1, cc - 1)) * cross_deriv_scale;
+        float tr = dxx + dyy;
+        float det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * edgeThreshold >= (edgeThreshold + 1) * (edgeThreshold + 1) * det) return 0;
+    }
+    kpt->x = ((float)*c + xc) * (float)(1 << octv);
+    kpt->y = ((float)*r + xr) * (float)(1 << octv);
+    kpt->octave = octv + (*layer << 8) + ((int)lrint((xi + 0.5) * 255) << 16);
+    kpt->size = sigma * (float)pow(2.0, (double)(((float)*layer + xi) / N_LAYERS)) * (float)(1 << octv) * 2;
+    kpt->response = fabsf(contr);
+    return 1;
+}
+
+static float calc_orientation_hist(const fimg_t* img, int px, int py, int radius, float sigma, float* hist)
+{
+    const int n = SIFT_ORI_HIST_BINS;
+    float expf_scale = -1.f / (2.f * sigma * sigma);
+    float th[SIFT_ORI_HIST_BINS + 4];
+    float* temphist = th + 2;
+    for (int i = 0; i < n; ++i) temphist[i] = 0.f;
+    for (int i = -radius; i <= radius; ++i) {
+        int y = py + i;
+        if (y <= 0 || y >= img->h - 1) continue;
+        for (int j = -radius; j <= radius; ++j) {
+            int x = px + j;
+            if (x <= 0 || x >= img->w - 1) continue;
+            float dx = AT(img, y, x + 1) - AT(img, y, x - 1);
+            float dy = AT(img, y - 1, x) - AT(img, y + 1, x);
+            float w = exp32f((float)(i * i + j * j) * expf_scale);
+            float ori = fast_atan2(dy, dx);
+            float mag = sqrtf(dx * dx + dy * dy);
+            int bin = (int)lrintf((n / 360.f) * ori);
+            if (bin >= n) bin -= n;
+            if (bin < 0) bin += n;
+            temphist[bin] += w * mag;
+        }
+    }
+    temphist[-1] = temphist[n - 1];
+    temphist[-2] = temphist[n - 2];
+    temphist[n] = temphist[0];
+    temphist[n + 1] = temphist[1];
+    for (int i = 0; i < n; ++i)
+        hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) + (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) +
+                  temphist[i] * (6.f / 16.f);
+    float maxval = hist[0];
+    for (int i = 1; i < n; ++i) maxval = maxval > hist[i] ? maxval : hist[i];
+    return maxval;
+}
+
+static void calc_descriptor(const fimg_t* img, float ptx, float pty, float ori, float scl, float* dst)
+{
+    const int d = SIFT_D, n = SIFT_N;
+    int ptix = (int)lrintf(ptx), ptiy = (int)lrintf(pty);
+    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180)));
+    float sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    float bins_per_rad = n / 360.f;
+    float exp_scale = -1.f / (d * d * 0.5f);
+    float hist_width = SIFT_DESCR_SCL_FCTR * scl;
+    int radius = (int)lrintf(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+    int rmax = (int)sqrt(((double)img->w) * img->w + ((double)img->h) * img->h);
+    if (radius > rmax) radius = rmax;
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    float hist[(SIFT_D + 2) * (SIFT_D + 2) * (SIFT_N + 2)];
+    memset(hist, 0, sizeof hist);
+    int rows = img->h, cols = img->w;
+    for (int i = -radius; i <= radius; ++i) {
+        for (int j = -radius; j <= radius; ++j) {
+            float c_rot = j * cos_t - i * sin_t;
+            float r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + d / 2 - 0.5f;
+            float cbin = c_rot + d / 2 - 0.5f;
+            int r = ptiy + i, c = ptix + j;
+            if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1))
+                continue;
+            float dx = AT(img, r, c + 1) - AT(img, r, c - 1);
+            float dy = AT(img, r - 1, c) - AT(img, r + 1, c);
+            float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+            float o = fast_atan2(dy, dx);
+            float mag = sqrtf(dx * dx + dy * dy) * wgt;
+            float obin = (o - ori) * bins_per_rad;
+            int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
+            rbin -= r0; cbin -= c0; obin -= o0;
+            if (o0 < 0) o0 += n;
+            if (o0 >= n) o0 -= n;
+            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+            hist[idx] += v_rco000;
+            hist[idx + 1] += v_rco001;
+            hist[idx + (n + 2)] += v_rco010;
+            hist[idx + (n + 3)] += v_rco011;
+            hist[idx + (d + 2) * (n + 2)] += v_rco100;
+            hist[idx + (d + 2) * (n + 2) + 1] += v_rco101;
+            hist[idx + (d + 3) * (n + 2)] += v_rco110;
+            hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
+        }
+    }
+    float raw[SIFT_D * SIFT_D * SIFT_N];
+    for (int i = 0; i < d; ++i)
+        for (int j = 0; j < d; ++j) {
+            int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+            hist[idx] += hist[idx + n];
+            hist[idx + 1] += hist[idx + n + 1];
+            for (int k = 0; k < n; ++k) raw[(i * d + j) * n + k] = hist[idx + k];
+        }
+    int len = d * d * n;
+    float nrm2 = 0;
+    for (int k = 0; k < len; ++k) nrm2 += raw[k] * raw[k];
+    float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
+    nrm2 = 0;
+    for (int i = 0; i < len; ++i) {
+        float v = raw[i] < thr ? raw[i] : thr;
+        raw[i] = v;
+        nrm2 += v * v;
+    }
+    float s = sqrtf(nrm2);
+    nrm2 = SIFT_INT_DESCR_FCTR / (s > FLT_EPSILON ? s : FLT_EPSILON);
+    for (int k = 0; k < len; ++k) {
+        float v = raw[k] * nrm2;
+        int iv = (int)lrintf(v);
+        dst[k] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
+    }
+}
+
+static int kp_less(const kp_t* a, const kp_t* b)
+{
+    if (a->x != b->x) return a->x < b->x;
+    if (a->y != b->y) return a->y < b->y;
+    if (a->size != b->size) return a->size > b->size;
+    if (a->angle != b->angle) return a->angle < b->angle;
+    if (a->response != b->response) return a->response > b->response;
+    if (a->octave != b->octave) return a->octave > b->octave;
+    return 0;
+}
+static int kp_cmp(const void* pa, const void* pb)
+{
+    const kp_t* a = (const kp_t*)pa;
+    const kp_t* b = (const kp_t*)pb;
+    if (kp_less(a, b)) return -1;
+    if (kp_less(b, a)) return 1;
+    return 0;
+}
+
+int vo_o_sift(const uint8_t* image, int w, int h, float* kp_out, float* desc, int cap, int* n_out)
+{
+    if (!image || w < 1 || h < 1 || !n_out) return VO_O_EARG;
+    exptab_init();
+    const double sigma = 1.6;
+    /* base: 2x upsample + blur to sigma */
+    fimg_t up = fimg_new(2 * w, 2 * h);
+    upsample2x(image, w, h, &up);
+    float sig_diff = sqrtf(fmaxf((float)(sigma * sigma) - 0.5f * 0.5f * 4, 0.01f));
+    fimg_t base = fimg_new(2 * w, 2 * h);
+    gauss_blur(&up, &base, sig_diff);
+    free(up.d);
+    int mn = base.w < base.h ? base.w : base.h;
+    int nOct = (int)lrint(log((double)mn) / log(2.) - 2) + 1;
+    double sig[N_LAYERS + 3];
+    sig[0] = sigma;
+    double k = pow(2., 1. / N_LAYERS);
+    for (int i = 1; i < N_LAYERS + 3; ++i) {
+        double sig_prev = pow(k, (double)(i - 1)) * sigma;
+        double sig_total = sig_prev * k;
+        sig[i] = sqrt(sig_total * sig_total - sig_prev * sig_prev);
+    }
+    fimg_t* gp = (fimg_t*)calloc((size_t)nOct * (N_LAYERS + 3), sizeof(fimg_t));
+    for (int o = 0; o < nOct; ++o)
+        for (int i = 0; i < N_LAYERS + 3; ++i) {
+            fimg_t* dst = &gp[o * (N_LAYERS + 3) + i];
+            if (o == 0 && i == 0) { *dst = base; continue; }
+            if (i == 0) {
+                const fimg_t* src = &gp[(o - 1) * (N_LAYERS + 3) + N_LAYERS];
+                *dst = fimg_new(src->w / 2, src->h / 2);
+                downsample_nn(src, dst);
+            } else {
+                const fimg_t* src = &gp[o * (N_LAYERS + 3) + i - 1];
+                *dst = fimg_new(src->w, src->h);
+                gauss_blur(src, dst, sig[i]);
+            }
+        }
+    fimg_t* dog = (fimg_t*)calloc((size_t)nOct * (N_LAYERS + 2), sizeof(fimg_t));
+    for (int o = 0; o < nOct; ++o)
+        for (int i = 0; i < N_LAYERS + 2; ++i) {
+            const fimg_t* a = &gp[o * (N_LAYERS + 3) + i];
+            const fimg_t* b = &gp[o * (N_LAYERS + 3) + i + 1];
+            fimg_t* d = &dog[o * (N_LAYERS + 2) + i];
+            *d = fimg_new(a->w, a->h);
+            for (size_t q = 0; q < (size_t)a->w * a->h; ++q) d->d[q] = b->d[q] - a->d[q];
+        }
+    /* extrema */
+    const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
+    size_t kcap = 1024, nk = 0;
+    kp_t* kps = (kp_t*)malloc(sizeof(kp_t) * kcap);
+    for (int o = 0; o < nOct; ++o)
+        for (int i = 1; i <= N_LAYERS; ++i) {
+            int idx = o * (N_LAYERS + 2) + i;
+            const fimg_t *img = &dog[idx], *prev = &dog[idx - 1], *next = &dog[idx + 1];
+            for (int r = SIFT_IMG_BORDER; r < img->h - SIFT_IMG_BORDER; ++r)
+                for (int c = SIFT_IMG_BORDER; c < img->w - SIFT_IMG_BORDER; ++c) {
+                    float val = AT(img, r, c);
+                    if (!(fabsf(val) > threshold)) continue;
+                    int ext = 1;
+                    for (int dz = 0; dz < 3 && ext; ++dz) {
+                        const fimg_t* L = dz == 0 ? prev : (dz == 1 ? img : next);
+                        for (int dy = -1; dy <= 1 && ext; ++dy)
+                            for (int dx = -1; dx <= 1; ++dx) {
+                                float u = AT(L, r + dy, c + dx);
+                                if (val > 0 ? !(val >= u) : !(val <= u)) { ext = 0; break; }
+                            }
+                    }
+                    if (!ext) continue;
+                    kp_t kpt;
+                    int r1 = r, c1 = c, layer = i;
+                    if (!adjust_local_extrema(dog, nOct, &kpt, o, &layer, &r1, &c1, (float)sigma)) continue;
+                    float scl_octv = kpt.size * 0.5f / (float)(1 << o);
+                    float hist[SIFT_ORI_HIST_BINS];
+                    float omax = calc_orientation_hist(&gp[o * (N_LAYERS + 3) + layer], c1, r1,
+                                                       (int)lrintf(SIFT_ORI_RADIUS * scl_octv),
+                                                       SIFT_ORI_SIG_FCTR * scl_octv, hist);
+                    float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
+                    const int n = SIFT_ORI_HIST_BINS;
+                    for (int j = 0; j < n; ++j) {
+                        int l = j > 0 ? j - 1 : n - 1;
+                        int r2 = j < n - 1 ? j + 1 : 0;
+                        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+                            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+                            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+                            kpt.angle = 360.f - (float)((360.f / n) * bin);
+                            if (fabsf(kpt.angle - 360.f) < FLT_EPSILON) kpt.angle = 0.f;
+                            if (nk == kcap) { kcap *= 2; kps = (kp_t*)realloc(kps, sizeof(kp_t) * kcap); }
+                            kps[nk++] = kpt;
+                        }
+                    }
+                }
+        }
+    /* removeDuplicatedSorted */
+    if (nk >= 2) {
+        qsort(kps, nk, sizeof(kp_t), kp_cmp);
+        size_t a = 0;
+        for (size_t b = 1; b < nk; ++b) {
+            const kp_t *k1 = &kps[a], *k2 = &kps[b];
+            if (k1->x != k2->x || k1->y != k2->y || k1->size != k2->size || k1->angle != k2->angle)
+                kps[++a] = kps[b];
+        }
+        nk = a + 1;
+    }
+    /* firstOctave = -1 adjustment */
+    for (size_t q = 0; q < nk; ++q) {
+        kps[q].octave = (kps[q].octave & ~255) | ((kps[q].octave - 1) & 255);
+        kps[q].x *= 0.5f;
+        kps[q].y *= 0.5f;
+        kps[q].size *= 0.5f;
+    }
+    *n_out = (int)nk;
+    int rc = VO_O_OK;
+    if ((int)nk > cap) rc = VO_O_ECAP;
+    for (size_t q = 0; q < nk && (int)q < cap; ++q) {
+        const kp_t* kp = &kps[q];
+        if (kp_out) {
+            kp_out[6 * q] = kp->x; kp_out[6 * q + 1] = kp->y; kp_out[6 * q + 2] = kp->size;
+            kp_out[6 * q + 3] = kp->angle; kp_out[6 * q + 4] = kp->response; kp_out[6 * q + 5] = (float)kp->octave;
+        }
+        if (desc) {
+            int octave = kp->octave & 255, layer = (kp->octave >> 8) & 255;
+            octave = octave < 128 ? octave : (-128 | octave);
+            float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+            float size = kp->size * scale;
+            float px = kp->x * scale, py = kp->y * scale;
+            const fimg_t* img = &gp[(octave + 1) * (N_LAYERS + 3) + layer];
+            float angle = 360.f - kp->angle;
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            calc_descriptor(img, px, py, angle, size * 0.5f, desc + 128 * q);
+        }
+    }
+    free(kps);
+    for (int q = 0; q < nOct * (N_LAYERS + 3); ++q) free(gp[q].d);
+    for (int q = 0; q < nOct * (N_LAYERS + 2); ++q) free(dog[q].d);
+    free(gp);
+    free(dog);
+    return rc;
+}
+
+int vo_o_bf_knn2(const float* q, int nq, const float* t, int nt, int dim, int32_t* idx2, float* dist2)
+{
+    if ((nq > 0 && !q) || (nt > 0 && !t) || !idx2 || !dist2) return VO_O_EARG;
+    for (int i = 0; i < nq; ++i) {
+        float d0 = FLT_MAX, d1 = FLT_MAX;
+        int i0 = -1, i1 = -1;
+        for (int j = 0; j < nt; ++j) {
+            float s = 0.f;
+            for (int k = 0; k < dim; ++k) {
+                float df = q[(size_t)i * dim + k] - t[(size_t)j * dim + k];
+                s += df * df;
+            }
+            float d = sqrtf(s);
+            if (d < d1) {
+                if (d0 > d) { d1 = d0; i1 = i0; d0 = d; i0 = j; }
+                else { d1 = d; i1 = j; }
+            }
+        }
+        idx2[2 * i] = i0; idx2[2 * i + 1] = i1;
+        dist2[2 * i] = d0; dist2[2 * i + 1] = d1;
+    }
+    return VO_O_OK;
+}

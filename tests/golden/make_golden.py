@@ -1,0 +1,105 @@
+"""Generate the golden fixtures that pin the orchestration (run in the build container).
+
+The reference VisualOdometryPipeLine class (/root/reference/VisualOdometryPipeLine.py)
+is imported *as is* with the CPU oracle shim (oracle/cv2_oracle.py) injected as
+``cv2``.  It is run on committed synthetic sequences (the generator is
+deterministic, so fixtures store frame digests, not frames) and every per-frame output
+the reference's driver reads (main.py:121-124,172-175) is saved, plus snapshots of the
+landmark / candidate arrays.  The reference never leaves this container; only these
+small .npz files travel.
+
+Usage:  python tests/golden/make_golden.py      (rewrites tests/golden/*.npz)
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+CASES = [
+    # name, sequence preset, seed, n_frames, snapshot frames
+    ("parking_c1", "parking", 0, 100, (6, 30, 60, 99)),
+    ("kitti_c2", "kitti", 1, 40, (2, 20, 39)),
+    ("malaga_c3", "malaga", 2, 24, (6, 23)),
+]
+
+
+def frame_digest(img: np.ndarray) -> np.ndarray:
+    return np.frombuffer(hashlib.sha1(np.ascontiguousarray(img).tobytes()).digest(), np.uint8)
+
+
+def run_reference(preset, seed, n_frames, snaps):
+    import oracle.cv2_oracle as cv2_oracle
+    sys.modules["cv2"] = cv2_oracle
+    sys.path.insert(0, "/root/reference")
+    import VisualOdometryPipeLine as ref  # the reference module, unmodified
+    from monocular_visual_odometry_va4mr_amd import options as O
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+
+    opts, boot, _ = O.get(preset)
+    frames, K, Rgt, cgt = make_sequence(preset, n_frames, seed=seed)
+    vo = ref.VisualOdometryPipeLine(K, opts)
+    rec = {k: [] for k in ("frame", "R", "t", "num_pts", "N", "P", "n_inl", "n_outl")}
+    snap = {}
+
+    def record(i):
+        R, t = vo.transforms[-1]
+        rec["frame"].append(i)
+        rec["R"].append(np.asarray(R, np.float64))
+        rec["t"].append(np.asarray(t, np.float64).reshape(3, 1))
+        rec["num_pts"].append(int(vo.num_pts[-1]))
+        rec["N"].append(len(vo.matched_landmarks))
+        rec["P"].append(int(vo.potential_keys.shape[0]))
+        rec["n_inl"].append(len(vo.inlier_pts_current))
+        rec["n_outl"].append(len(vo.outlier_pts_current))
+        if i in snaps:
+            snap[f"lm_{i}"] = np.asarray(vo.matched_landmarks, np.float32)
+            snap[f"kp_{i}"] = np.asarray(vo.matched_keypoints, np.float32)
+            snap[f"cand_{i}"] = np.asarray(vo.potential_keys, np.float32)
+            snap[f"cand_first_{i}"] = np.asarray(vo.potential_first_keys, np.float32)
+            snap[f"cand_tau_{i}"] = np.asarray(vo.potential_transforms, np.float64)
+
+    t0 = time.perf_counter()
+    vo.initialization(frames[boot[0]], frames[boot[1]])
+    record(boot[1])
+    error = ""
+    for i in range(boot[1] + 1, n_frames):           # main.py:166
+        try:
+            vo.continuous_operation(frames[i])
+        except Exception as e:                       # the reference crashes here; record it
+            error = f"{type(e).__name__}: {e}"
+            break
+        record(i)
+    dt = time.perf_counter() - t0
+    out = {k: np.asarray(v) for k, v in rec.items()}
+    out.update(snap)
+    out["digests"] = np.stack([frame_digest(f) for f in frames])
+    out["K"] = K
+    out["boot"] = np.asarray(boot)
+    out["gt_R"] = Rgt
+    out["gt_c"] = cgt
+    out["error"] = np.asarray(error)
+    return out, dt
+
+
+def main():
+    for name, preset, seed, n, snaps in CASES:
+        out, dt = run_reference(preset, seed, n, snaps)
+        out["preset"] = np.asarray(preset)
+        out["seed"] = np.asarray(seed)
+        out["n_frames"] = np.asarray(n)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        print(f"{name}: {len(out['frame'])} frames recorded in {dt:.1f}s, error={out['error']!r}, "
+              f"{os.path.getsize(path) / 1024:.0f} KiB")
+
+
+if __name__ == "__main__":
+    main()
