@@ -1,0 +1,230 @@
+/*
+ * vo_hip.h -- C ABI of libvo_hip.so, the MI355X (gfx950) VO hot path.
+ *
+ * Drop-in boundary.  The reference has no FFI: its hot path sits behind
+ * (B1) nine cv2 calls made by /root/reference/VisualOdometryPipeLine.py and (B2) the
+ * VisualOdometryPipeLine class itself.  Each entry point below names the reference
+ * call it replaces.  The library never allocates on a call path: every buffer is a
+ * caller-owned device pointer (PyTorch tensors are used purely as containers), every
+ * call is asynchronous on the given HIP stream, returns an int status (0 = OK,
+ * VO_E* < 0 on bad arguments / HIP launch errors) and leaves per-chain runtime
+ * outcomes (the reference's ValueError conditions) in the device status word.
+ *
+ * Batching: B independent VO chains ("shards") are processed per call.  State arrays
+ * are [B][capacity] with per-chain device counts, so a whole per-frame step is a fixed
+ * sequence of launches with no host synchronisation (hipGraph-capturable).
+ */
+#ifndef VO_HIP_H
+#define VO_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vo_stream_t; /* hipStream_t */
+
+enum vo_err {
+    VO_OK = 0,
+    VO_EARG = -1,
+    VO_EHIP = -2,
+};
+
+/* per-chain runtime status (device int32), set by the stage that detects it */
+enum vo_chain_status {
+    VO_ST_OK = 0,
+    VO_ST_NOT_ENOUGH_KP = 1,   /* VisualOdometryPipeLine.py:357-358 ValueError      */
+    VO_ST_PNP_FAILED = 2,      /* VisualOdometryPipeLine.py:351-352 ValueError      */
+    VO_ST_GFTT_NONE = 3,       /* :256 goodFeaturesToTrack returned None -> crash  */
+    VO_ST_GFTT_ONE = 4,        /* :256-258 single corner -> squeeze() breaks index */
+    VO_ST_CAPACITY = 5,        /* a fixed capacity of this engine was exceeded     */
+    VO_ST_ESSENTIAL_FAILED = 6,/* :308 findEssentialMat produced no model          */
+    VO_ST_NO_MATCHES = 7,      /* :209-245 no bootstrap matches                    */
+};
+
+#define VO_MAX_LEVELS 8
+#define VO_BORDER 16
+
+/* Geometry of the per-chain image pyramid (u8 images with a VO_BORDER reflect-101
+ * border; derivative images short2 with a zero border, same pitch in elements). */
+typedef struct vo_dims {
+    int32_t B, W, H;
+    int32_t nlev;                 /* levels kept (maxLevel + 1 after the winSize cap)   */
+    int32_t lvl_w[VO_MAX_LEVELS], lvl_h[VO_MAX_LEVELS], lvl_pitch[VO_MAX_LEVELS];
+    int64_t lvl_off[VO_MAX_LEVELS];  /* byte offset of level l (padded origin)         */
+    int64_t pyr_stride;           /* bytes per chain, u8 pyramid                          */
+    int64_t der_stride;           /* elements (int16) per chain, derivative pyramid       */
+    int32_t ncap, pcap, fcap;     /* landmark, candidate, pose capacities per chain       */
+    int32_t ccap;                 /* GFTT local-maximum candidates per chain              */
+    int32_t mcap;                 /* GFTT output corners per chain                        */
+    int64_t work_stride;          /* fp64 scratch per chain (>= 16*max(ncap,pcap)+4096)   */
+    int64_t iwork_stride;         /* int32 scratch per chain (>= 2*max(ncap,pcap)+4096)   */
+} vo_dims;
+
+/* Reference options (main.py:20-44 keys) plus host-derived constants. */
+typedef struct vo_opts {
+    double K[9], K_inv[9];
+    double min_dist_landmarks, max_dist_landmarks;
+    double min_baseline_angle;    /* degrees                                            */
+    double cos_baseline;          /* cos(radians(min_baseline_angle)), host-computed    */
+    int32_t min_baseline_frames;
+    double feature_ratio;
+    int32_t feature_max_corners;
+    double feature_quality_level, feature_min_dist;
+    int32_t feature_block_size, feature_use_harris;
+    double harris_k;
+    int32_t win_w, win_h, max_level, crit_type, crit_count;
+    double crit_eps;              /* raw epsilon (squared inside, as OpenCV)             */
+    double min_eig;
+    double pnp_conf, pnp_error;
+    int32_t pnp_iters;
+} vo_opts;
+
+/* Device state of B chains; every pointer is [B][...] contiguous per chain. */
+typedef struct vo_state {
+    uint8_t* pyr[2];              /* ping-pong image pyramids  [B][pyr_stride]          */
+    int16_t* der;                 /* Scharr of the previous frame [B][der_stride]       */
+    float* lm_X;                  /* matched_landmarks  [B][ncap][3]                     */
+    float* lm_kp;                 /* matched_keypoints  [B][ncap][2]                     */
+    int32_t* nL;                  /* [B]                                                 */
+    float* c_kp;                  /* potential_keys       [B][pcap][2]                   */
+    float* c_first;               /* potential_first_keys [B][pcap][2]                   */
+    int32_t* c_tau;               /* potential_transforms [B][pcap]                      */
+    int32_t* nC;                  /* [B]                                                 */
+    double* pose_R;               /* transforms (R_CW)  [B][fcap][9]                     */
+    double* pose_t;               /* transforms (t_CW)  [B][fcap][3]                     */
+    int32_t* nF;                  /* len(transforms) [B]                                 */
+    int32_t* num_pts;             /* [B][fcap]                                           */
+    float* outl_kp;               /* outlier_pts_current [B][max(ncap,pcap)][2]          */
+    float* inl_kp;                /* inlier_pts_current  [B][max(ncap,pcap)][2]          */
+    int32_t* nOutl;               /* [B]                                                 */
+    int32_t* nInl;                /* len(inlier_pts_current) [B]                         */
+    int32_t* status;              /* enum vo_chain_status [B]                            */
+    /* scratch */
+    float* trk_pts;               /* LK outputs [B][ncap+pcap][2]                        */
+    uint8_t* trk_st;              /* LK status  [B][ncap+pcap]                           */
+    float* trk_err;               /* LK err     [B][ncap+pcap]                           */
+    float* eig;                   /* GFTT eigen map [B][W*H]                              */
+    uint32_t* eig_max;            /* [B] order-preserving float bits                      */
+    uint64_t* gf_keys;            /* [B][ccap]                                            */
+    int32_t* gf_n;                /* [B]                                                  */
+    float* corners;               /* [B][mcap][2]                                         */
+    int32_t* nCorners;            /* [B]                                                  */
+    double* pnp_rt;               /* PnP rvec,tvec [B][6]                                 */
+    int32_t* pnp_ok;              /* PnP success [B]                                      */
+    int32_t* pnp_ninl;            /* PnP inlier count [B]                                 */
+    uint8_t* pnp_mask;            /* PnP inlier mask [B][ncap]                            */
+    double* work;                 /* per-chain fp64 scratch [B][work_stride]              */
+    int32_t* iwork;               /* per-chain int scratch  [B][iwork_stride]             */
+} vo_state;
+
+/* ---- library ---------------------------------------------------------------- */
+const char* vo_version(void);
+int vo_device_arch(char* buf, int len);          /* gcnArchName of the current device */
+
+/* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
+
+/* Build the pyramid of the new frames into state->pyr[cur] (part of cv2.calcOpticalFlowPyrLK,
+ * :281,287).  frames: [B][H][W] u8, frame_stride bytes between chains. */
+int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
+                 int64_t frame_stride, vo_stream_t stream);
+/* Scharr derivatives of pyramid `which` into state->der (calcSharrDeriv). */
+int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t stream);
+
+/* feature_tracking (:271-290): LK of landmarks and (if P > 1) candidates from pyr[prev]
+ * to pyr[1-prev], then the reference's status filtering (ordered compaction). */
+int vo_track(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, vo_stream_t stream);
+
+/* PnP step (:338-358): guard N >= 8, cv2.solvePnPRansac(P3P) + EPnP refit, inlier
+ * filtering, Rodrigues, inversion; writes pose slot nF (not yet counted). */
+int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
+
+/* triangulate_landmarks (:107-206) incl. cv2.triangulatePoints per candidate (:188),
+ * using pose slot nF as the current pose.  Runs only where P > 1 (:366) unless force. */
+int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force,
+                   vo_stream_t stream);
+
+/* cv2.goodFeaturesToTrack (:256) on pyramid level 0 of pyr[cur] -> state->corners. */
+int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream);
+
+/* feature_adding distance filter + append (:258-268) and the pose/num_pts append
+ * (:371-373).  Call after vo_gftt. */
+int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
+
+/* ---- single-call primitives for the cv2 surface (B1) --------------------------- */
+
+/* cv2.calcOpticalFlowPyrLK (:281,287): points [B][n] with per-chain counts, using the
+ * pyramids/derivatives already in state (prev = pyr[prev], next = pyr[1-prev]). */
+int vo_lk_points(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev,
+                 const float* pts, const int32_t* counts, int32_t cap, float* out_pts,
+                 uint8_t* out_status, float* out_err, vo_stream_t stream);
+
+/* cv2.solvePnPRansac(..., SOLVEPNP_P3P) (:343) on [B][cap] points with counts.
+ * out: rvec[B][3], tvec[B][3], success[B], inlier mask [B][cap] (u8), n_inl[B]. */
+int vo_pnp_ransac(const vo_opts* o, int B, const float* obj, const float* img,
+                  const int32_t* counts, int32_t cap, double* rvec, double* tvec,
+                  int32_t* success, uint8_t* inl_mask, int32_t* n_inl, double* work,
+                  int64_t work_stride, vo_stream_t stream);
+
+/* cv2.triangulatePoints (:188) for float32 points: P1,P2 [n][12] (row-major 3x4 each,
+ * one pair per point), x1,x2 [n][2] -> out [n][4] float32. */
+int vo_triangulate_points(int n, const double* P1, const double* P2, const float* x1,
+                          const float* x2, float* out4, vo_stream_t stream);
+
+/* cv2.Rodrigues (:354): n vectors [n][3] -> matrices [n][9], or the inverse. */
+int vo_rodrigues(int n, int to_matrix, const double* in, double* out, vo_stream_t stream);
+
+/* ---- bootstrap (initialization, :293-323) --------------------------------------- */
+
+typedef struct vo_sift_buf {
+    float* gauss;                 /* octave-layer Gaussian images, packed              */
+    float* dog;                   /* DoG images, packed                                */
+    float* tmp;                   /* blur scratch                                      */
+    int64_t gauss_off[16 * 6], dog_off[16 * 5];
+    int32_t oct_w[16], oct_h[16];
+    int32_t n_oct;
+    float* kern;                  /* Gaussian kernels [6][64] (host-computed, exp())   */
+    int32_t ksize[6];
+    float* exptab;                /* exp32f table [64]                                 */
+    int32_t* cand;                /* extrema candidates [cand_cap][4]                  */
+    int32_t* n_cand;
+    float* kp;                    /* raw keypoints [kp_cap][8]                         */
+    int32_t* n_kp;
+    int32_t* order;               /* sort permutation [kp_cap]                         */
+    float* kp_out;                /* sorted, deduplicated keypoints [kp_cap][6]        */
+    float* desc;                  /* descriptors [kp_cap][128]                         */
+    int32_t* n_out;
+    float* hist_scratch;          /* [kp_cap][360]                                     */
+    int32_t cand_cap, kp_cap;
+} vo_sift_buf;
+
+/* cv2.SIFT_create().detectAndCompute(img, None) (:35,226-227) for one image. */
+int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream);
+
+/* BFMatcher().knnMatch(q, t, k=2) (:36,229): integer-valued float descriptors,
+ * MFMA distance matrix; out idx [nq][2], dist [nq][2]. counts read on device. */
+int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt,
+               int32_t qcap, int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream);
+
+/* cv2.findEssentialMat(p0,p1,K,RANSAC,prob,threshold) (:308) for B problems of
+ * [B][cap] points with counts; E [B][9], mask [B][cap]. */
+int vo_find_essential(const vo_opts* o, int B, const float* p0, const float* p1,
+                      const int32_t* counts, int32_t cap, double prob, double threshold,
+                      int32_t max_iters, double* E, uint8_t* mask, int32_t* ok, double* work,
+                      int32_t work_doubles, vo_stream_t stream);
+
+/* cv2.recoverPose(E,p0,p1,K) (:315): R [B][9], t [B][3], mask [B][cap], n_good [B]. */
+int vo_recover_pose(const vo_opts* o, int B, const double* E, const float* p0,
+                    const float* p1, const int32_t* counts, int32_t cap, double* R, double* t,
+                    uint8_t* mask, int32_t* n_good, vo_stream_t stream);
+
+/* Bootstrap assembly into chain state (initial_feature_matching + :308-323): from the
+ * per-chain bootstrap matches (pts0/pts1 [B][cap], counts) run E-RANSAC, inlier
+ * filtering, recoverPose, sign fix, triangulation, pose append, num_pts. */
+int vo_bootstrap(const vo_dims* d, const vo_opts* o, const vo_state* s, const float* pts0,
+                 const float* pts1, const int32_t* counts, int32_t cap, vo_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

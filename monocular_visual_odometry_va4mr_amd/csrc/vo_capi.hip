@@ -1,0 +1,18 @@
+// Library-level C ABI entry points of libvo_hip.so (see include/vo_hip.h).
+#include "vo_dev.h"
+
+#include <string.h>
+
+extern "C" const char* vo_version(void) { return "vo_hip 0.1 (gfx950)"; }
+
+extern "C" int vo_device_arch(char* buf, int len)
+{
+    if (!buf || len <= 0) return VO_EARG;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return VO_EHIP;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return VO_EHIP;
+    strncpy(buf, p.gcnArchName, (size_t)len - 1);
+    buf[len - 1] = 0;
+    return VO_OK;
+}

@@ -1,0 +1,85 @@
+// Device helpers shared by the gfx950 kernels of libvo_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vo_hip.h"
+
+#define VO_DEV __device__ __forceinline__
+
+VO_DEV int lane_id() { return threadIdx.x & 63; }
+VO_DEV int wave_id() { return threadIdx.x >> 6; }
+
+// BORDER_REFLECT_101 index (cv::borderInterpolate)
+VO_DEV int refl101(int p, int len)
+{
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = (p < 0) ? -p : 2 * len - p - 2;
+    return p;
+}
+
+VO_DEV int64_t wave_sum_i64(int64_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+VO_DEV int wave_sum_i32(int v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// exclusive prefix of a per-thread flag over the whole block; lds must hold 16 ints
+VO_DEV int block_scan_flag(bool f, int* lds, int* total)
+{
+    unsigned long long m = __ballot(f);
+    const int lane = lane_id(), w = wave_id(), nw = blockDim.x >> 6;
+    int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) lds[w] = __popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < nw; ++i) {
+        int c = lds[i];
+        if (i < w) base += c;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + pre;
+}
+
+// sum of an int over the block; lds must hold 16 ints
+VO_DEV int block_sum_i32(int v, int* lds)
+{
+    v = wave_sum_i32(v);
+    if (lane_id() == 0) lds[wave_id()] = v;
+    __syncthreads();
+    int t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += lds[i];
+    __syncthreads();
+    return t;
+}
+
+// order-preserving map float -> uint32 (larger float -> larger key)
+VO_DEV uint32_t fkey(float f)
+{
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+VO_DEV float fkey_inv(uint32_t k)
+{
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return __uint_as_float(u);
+}
+
+// cv::RNG::next()
+VO_DEV uint32_t rng_next(uint64_t& s)
+{
+    s = (uint64_t)(uint32_t)s * 4164903690ULL + (s >> 32);
+    return (uint32_t)s;
+}
+
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))

@@ -1,0 +1,748 @@
+// Image-side kernels for gfx950: pyramid ingest + pyrDown, Scharr derivatives,
+// pyramidal Lucas-Kanade (one 64-lane wave per point), tracking compaction, and
+// goodFeaturesToTrack (integer-exact min-eigenvalue map, 3x3 NMS, paged radix-select +
+// LDS bitonic sort, wave-parallel greedy min-distance selection).
+//
+// Reference call sites: VisualOdometryPipeLine.py:256 (goodFeaturesToTrack),
+// :281,:287 (calcOpticalFlowPyrLK).  Arithmetic follows oracle/vo_oracle_img.c
+// operation by operation (that file restates OpenCV 4.6), so the
+// integer stages are bit-exact and the float stages use the same op order (built with
+// -ffp-contract=off, correctly rounded f32 div/sqrt).
+#include "vo_dev.h"
+
+#include <float.h>
+
+namespace {
+
+// ------------------------------------------------------------------ pyramid
+__global__ void k_ingest(const uint8_t* __restrict__ frames, int64_t fstride, uint8_t* __restrict__ pyr,
+                         int64_t pstride, int W, int H, int pitch, int64_t off)
+{
+    const int b = blockIdx.z;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y;
+    if (px >= W + 2 * VO_BORDER) return;
+    const int sx = refl101(px - VO_BORDER, W), sy = refl101(py - VO_BORDER, H);
+    pyr[b * pstride + off + (int64_t)py * pitch + px] = frames[b * fstride + (int64_t)sy * W + sx];
+}
+
+__global__ void k_pyrdown(uint8_t* __restrict__ pyr, int64_t pstride, int sw, int spitch, int64_t soff,
+                          int dw, int dh, int dpitch, int64_t doff)
+{
+    const int b = blockIdx.z;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y;
+    if (px >= dw + 2 * VO_BORDER) return;
+    const int ix = refl101(px - VO_BORDER, dw), iy = refl101(py - VO_BORDER, dh);
+    const uint8_t* src = pyr + b * pstride + soff;
+    // source reads stay inside the source's reflect-101 border (|offset| <= 2 < VO_BORDER)
+    const int k5[5] = {1, 4, 6, 4, 1};
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint8_t* row = src + (int64_t)(2 * iy - 2 + i + VO_BORDER) * spitch + (2 * ix - 2 + VO_BORDER);
+        int r = row[0] + 4 * row[1] + 6 * row[2] + 4 * row[3] + row[4];
+        acc += k5[i] * r;
+    }
+    (void)sw;
+    pyr[b * pstride + doff + (int64_t)py * dpitch + px] = (uint8_t)((acc + 128) >> 8);
+}
+
+__global__ void k_scharr(const uint8_t* __restrict__ pyr, int64_t pstride, int16_t* __restrict__ der,
+                         int64_t dstride, int w, int h, int pitch, int64_t off)
+{
+    const int b = blockIdx.z;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x;
+    const int py = blockIdx.y;
+    if (px >= w + 2 * VO_BORDER) return;
+    int16_t* d = der + b * dstride + 2 * (off + (int64_t)py * pitch + px);
+    const int x = px - VO_BORDER, y = py - VO_BORDER;
+    if (x < 0 || x >= w || y < 0 || y >= h) {
+        d[0] = 0;
+        d[1] = 0;
+        return;
+    }
+    const uint8_t* c = pyr + b * pstride + off + (int64_t)py * pitch + px;
+    const uint8_t* u = c - pitch;   // reflect-101 border rows/cols are materialised
+    const uint8_t* l = c + pitch;
+    int t0l = (u[-1] + l[-1]) * 3 + c[-1] * 10;
+    int t0r = (u[1] + l[1]) * 3 + c[1] * 10;
+    int t1l = l[-1] - u[-1], t1c = l[0] - u[0], t1r = l[1] - u[1];
+    d[0] = (int16_t)(t0r - t0l);
+    d[1] = (int16_t)((t1r + t1l) * 3 + t1c * 10);
+}
+
+// ------------------------------------------------------------------ LK
+struct LKParams {
+    const uint8_t* prev;
+    const int16_t* der;
+    const uint8_t* next;
+    int64_t pstride, dstride;
+    int L;                          // top level used
+    int lw[VO_MAX_LEVELS], lh[VO_MAX_LEVELS], lpitch[VO_MAX_LEVELS];
+    int64_t loff[VO_MAX_LEVELS];
+    int win_w, win_h, max_count;
+    double eps2;
+    float min_eig;
+    // point segments: seg0 then seg1 (seg1 used only where its count > seg1_min)
+    const float* p0;
+    const int32_t* n0;
+    int cap0;
+    const float* p1;
+    const int32_t* n1;
+    int cap1;
+    int seg1_min;
+    const int32_t* chain_status;
+    float* out;
+    uint8_t* st;
+    float* err;
+    int ocap;
+};
+
+template <int MAXJ>
+__global__ void __launch_bounds__(256) k_lk(LKParams P)
+{
+    const int b = blockIdx.y;
+    if (P.chain_status && P.chain_status[b] != 0) return;
+    const int lane = lane_id();
+    const int n0 = P.n0 ? P.n0[b] : 0;
+    int n1 = P.n1 ? P.n1[b] : 0;
+    if (n1 <= P.seg1_min) n1 = 0;
+    const int ntot = n0 + n1;
+    const int ww = P.win_w, wh = P.win_h, npx = ww * wh;
+    const float hx = (ww - 1) * 0.5f, hy = (wh - 1) * 0.5f;
+    const int wpb = blockDim.x >> 6;
+    for (int p = blockIdx.x * wpb + wave_id(); p < ntot; p += gridDim.x * wpb) {
+        const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
+        const float ptx = src[0], pty = src[1];
+        int status = 1;
+        float errv = 0.f;
+        float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
+        for (int level = P.L; level >= 0; --level) {
+            const int cols = P.lw[level], rows = P.lh[level], pitch = P.lpitch[level];
+            const uint8_t* I = P.prev + b * P.pstride + P.loff[level];
+            const int16_t* DI = P.der + b * P.dstride + 2 * P.loff[level];
+            const uint8_t* J = P.next + b * P.pstride + P.loff[level];
+            const float sc = (float)(1. / (1 << level));
+            float px = ptx * sc, py = pty * sc;
+            if (level == P.L) { ox = px; oy = py; }
+            else { ox = ox * 2.f; oy = oy * 2.f; }
+            px -= hx;
+            py -= hy;
+            const int ipx = (int)floorf(px), ipy = (int)floorf(py);
+            if (ipx < -ww || ipx >= cols || ipy < -wh || ipy >= rows) {
+                if (level == 0) { status = 0; errv = 0.f; }
+                continue;
+            }
+            float a = px - ipx, bb = py - ipy;
+            int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
+            int iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
+            int iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
+            int iw11 = (1 << 14) - iw00 - iw01 - iw10;
+            int ival[MAXJ], ixv[MAXJ], iyv[MAXJ];
+            int a11 = 0, a12 = 0, a22 = 0;
+#pragma unroll
+            for (int j = 0; j < MAXJ; ++j) {
+                const int k = lane + 64 * j;
+                ival[j] = 0; ixv[j] = 0; iyv[j] = 0;
+                if (k < npx) {
+                    const int wy = k / ww, wx = k - wy * ww;
+                    const int64_t o = (int64_t)(ipy + wy + VO_BORDER) * pitch + (ipx + wx + VO_BORDER);
+                    const uint8_t* s = I + o;
+                    ival[j] = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9);
+                    const int16_t* d = DI + 2 * o;
+                    const int ds = 2 * pitch;
+                    ixv[j] = DESCALE(d[0] * iw00 + d[2] * iw01 + d[ds] * iw10 + d[ds + 2] * iw11, 14);
+                    iyv[j] = DESCALE(d[1] * iw00 + d[3] * iw01 + d[ds + 1] * iw10 + d[ds + 3] * iw11, 14);
+                    a11 += ixv[j] * ixv[j];
+                    a12 += ixv[j] * iyv[j];
+                    a22 += iyv[j] * iyv[j];
+                }
+            }
+            const int64_t iA11 = wave_sum_i64(a11), iA12 = wave_sum_i64(a12), iA22 = wave_sum_i64(a22);
+            const float FLT_SCALE = 1.f / (1 << 20);
+            const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
+            float D = A11 * A22 - A12 * A12;
+            const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * ww * wh);
+            if (minEig < P.min_eig || D < FLT_EPSILON) {
+                if (level == 0) status = 0;
+                continue;
+            }
+            D = 1.f / D;
+            float nx = ox - hx, ny = oy - hy;
+            float pdx = 0.f, pdy = 0.f;
+            for (int it = 0; it < P.max_count; ++it) {
+                const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+                if (inx < -ww || inx >= cols || iny < -wh || iny >= rows) {
+                    if (level == 0) status = 0;
+                    break;
+                }
+                a = nx - inx;
+                bb = ny - iny;
+                iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
+                iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
+                iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
+                iw11 = (1 << 14) - iw00 - iw01 - iw10;
+                int b1 = 0, b2 = 0;
+#pragma unroll
+                for (int j = 0; j < MAXJ; ++j) {
+                    const int k = lane + 64 * j;
+                    if (k < npx) {
+                        const int wy = k / ww, wx = k - wy * ww;
+                        const uint8_t* s = J + (int64_t)(iny + wy + VO_BORDER) * pitch + (inx + wx + VO_BORDER);
+                        const int diff = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9) - ival[j];
+                        b1 += diff * ixv[j];
+                        b2 += diff * iyv[j];
+                    }
+                }
+                const float fb1 = (float)wave_sum_i64(b1) * FLT_SCALE;
+                const float fb2 = (float)wave_sum_i64(b2) * FLT_SCALE;
+                const float ddx = (A12 * fb2 - A22 * fb1) * D;
+                const float ddy = (A12 * fb1 - A11 * fb2) * D;
+                nx += ddx;
+                ny += ddy;
+                ox = nx + hx;
+                oy = ny + hy;
+                if ((double)ddx * ddx + (double)ddy * ddy <= P.eps2) break;
+                if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
+                    ox -= ddx * 0.5f;
+                    oy -= ddy * 0.5f;
+                    break;
+                }
+                pdx = ddx;
+                pdy = ddy;
+            }
+            if (status && level == 0) {
+                const float fx = ox - hx, fy = oy - hy;
+                const int inx = (int)floorf(fx), iny = (int)floorf(fy);
+                if (inx < -ww || inx >= cols || iny < -wh || iny >= rows) {
+                    status = 0;
+                    continue;
+                }
+                const float aa = fx - inx, cc = fy - iny;
+                iw00 = __float2int_rn((1.f - aa) * (1.f - cc) * (float)(1 << 14));
+                iw01 = __float2int_rn(aa * (1.f - cc) * (float)(1 << 14));
+                iw10 = __float2int_rn((1.f - aa) * cc * (float)(1 << 14));
+                iw11 = (1 << 14) - iw00 - iw01 - iw10;
+                int es = 0;
+#pragma unroll
+                for (int j = 0; j < MAXJ; ++j) {
+                    const int k = lane + 64 * j;
+                    if (k < npx) {
+                        const int wy = k / ww, wx = k - wy * ww;
+                        const uint8_t* s = J + (int64_t)(iny + wy + VO_BORDER) * pitch + (inx + wx + VO_BORDER);
+                        const int diff = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9) - ival[j];
+                        es += diff < 0 ? -diff : diff;
+                    }
+                }
+                errv = (float)wave_sum_i32(es) / (float)(32 * ww * wh);
+            }
+        }
+        if (lane == 0) {
+            const int64_t o = (int64_t)b * P.ocap + p;
+            P.out[2 * o] = ox;
+            P.out[2 * o + 1] = oy;
+            P.st[o] = (uint8_t)status;
+            if (P.err) P.err[o] = errv;
+        }
+    }
+}
+
+// ---------------------------------------------------- tracking compaction (:282-290)
+__global__ void __launch_bounds__(256) k_track_compact(vo_dims d, vo_state s)
+{
+    __shared__ int lds[16];
+    const int b = blockIdx.x;
+    if (s.status[b] != 0) return;
+    const int nL = s.nL[b], nC = s.nC[b];
+    const int ocap = d.ncap + d.pcap;
+    const float* tp = s.trk_pts + (int64_t)b * ocap * 2;
+    const uint8_t* ts = s.trk_st + (int64_t)b * ocap;
+    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    int out = 0;
+    for (int base = 0; base < nL; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool ok = i < nL && ts[i] == 1;
+        float x0 = 0, x1 = 0, x2 = 0, k0 = 0, k1 = 0;
+        if (ok) { x0 = X[3 * i]; x1 = X[3 * i + 1]; x2 = X[3 * i + 2]; k0 = tp[2 * i]; k1 = tp[2 * i + 1]; }
+        int tot;
+        const int pos = out + block_scan_flag(ok, lds, &tot);
+        if (ok) { X[3 * pos] = x0; X[3 * pos + 1] = x1; X[3 * pos + 2] = x2; kp[2 * pos] = k0; kp[2 * pos + 1] = k1; }
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s.nL[b] = out;
+    if (nC <= 1) return;   // quirk Q7: a single candidate is neither tracked nor filtered
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    out = 0;
+    for (int base = 0; base < nC; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool ok = i < nC && ts[nL + i] == 1;
+        float k0 = 0, k1 = 0, f0 = 0, f1 = 0;
+        int tau = 0;
+        if (ok) { k0 = tp[2 * (nL + i)]; k1 = tp[2 * (nL + i) + 1]; f0 = cf[2 * i]; f1 = cf[2 * i + 1]; tau = ct[i]; }
+        int tot;
+        const int pos = out + block_scan_flag(ok, lds, &tot);
+        if (ok) { ck[2 * pos] = k0; ck[2 * pos + 1] = k1; cf[2 * pos] = f0; cf[2 * pos + 1] = f1; ct[pos] = tau; }
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s.nC[b] = out;
+}
+
+// ------------------------------------------------------------------ GFTT
+struct EigParams {
+    const uint8_t* pyr;
+    int64_t pstride;
+    int W, H, pitch;
+    int64_t off;
+    int bs, harris;
+    double harris_k;
+    float* eig;
+    uint32_t* eig_max;
+    const int32_t* chain_status;
+};
+
+#define EIG_T 16
+#define EIG_MAXBS 7
+__global__ void __launch_bounds__(256) k_eig(EigParams P)
+{
+    __shared__ int sdx[(EIG_T + EIG_MAXBS - 1) * (EIG_T + EIG_MAXBS - 1)];
+    __shared__ int sdy[(EIG_T + EIG_MAXBS - 1) * (EIG_T + EIG_MAXBS - 1)];
+    __shared__ uint32_t smax;
+    const int b = blockIdx.z;
+    if (P.chain_status && P.chain_status[b] != 0) return;
+    const int bs = P.bs, a0 = bs / 2, tw = EIG_T + bs - 1;
+    const int x0 = blockIdx.x * EIG_T, y0 = blockIdx.y * EIG_T;
+    const uint8_t* img = P.pyr + b * P.pstride + P.off;
+    if (threadIdx.x == 0) smax = 0;
+    for (int q = threadIdx.x; q < tw * tw; q += blockDim.x) {
+        const int ty = q / tw, tx = q - ty * tw;
+        // box-filter taps reflect on the covariance image, then Sobel reads the
+        // reflect-101 border of the padded level-0 image
+        const int cx = refl101(x0 - a0 + tx, P.W), cy = refl101(y0 - a0 + ty, P.H);
+        const uint8_t* c = img + (int64_t)(cy + VO_BORDER) * P.pitch + (cx + VO_BORDER);
+        const uint8_t* u = c - P.pitch;
+        const uint8_t* l = c + P.pitch;
+        sdx[q] = (u[1] - u[-1]) + 2 * (c[1] - c[-1]) + (l[1] - l[-1]);
+        sdy[q] = (l[-1] - u[-1]) + 2 * (l[0] - u[0]) + (l[1] - u[1]);
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & (EIG_T - 1), ty = threadIdx.x / EIG_T;
+    const int x = x0 + tx, y = y0 + ty;
+    if (x < P.W && y < P.H) {
+        int sxx = 0, sxy = 0, syy = 0;
+        for (int i = 0; i < bs; ++i)
+            for (int j = 0; j < bs; ++j) {
+                const int q = (ty + i) * tw + (tx + j);
+                const int gx = sdx[q], gy = sdy[q];
+                sxx += gx * gx;
+                sxy += gx * gy;
+                syy += gy * gy;
+            }
+        const double s = 1.0 / ((double)(1 << 2) * bs * 255.0);
+        float v;
+        if (!P.harris) {
+            const int64_t T = (int64_t)sxx + syy;
+            const int64_t dd = (int64_t)sxx - syy;
+            const int64_t Dd = dd * dd + 4 * (int64_t)sxy * sxy;
+            const double lam = ((double)T - sqrt((double)Dd)) * (s * s * 0.5);
+            v = (float)lam;
+        } else {
+            const int64_t det = (int64_t)sxx * syy - (int64_t)sxy * sxy;
+            const int64_t T = (int64_t)sxx + syy;
+            const double r = ((double)det - P.harris_k * (double)(T * T)) * (s * s * s * s);
+            v = (float)r;
+        }
+        P.eig[(int64_t)b * P.W * P.H + (int64_t)y * P.W + x] = v;
+        atomicMax(&smax, fkey(v));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&P.eig_max[b], smax);
+}
+
+struct NmsParams {
+    const float* eig;
+    const uint32_t* eig_max;
+    int W, H;
+    double quality;
+    uint64_t* keys;
+    int32_t* nkeys;
+    int ccap;
+    const int32_t* chain_status;
+};
+
+__global__ void __launch_bounds__(256) k_nms(NmsParams P)
+{
+    const int b = blockIdx.z;
+    if (P.chain_status && P.chain_status[b] != 0) return;
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const float thr = (float)((double)fkey_inv(P.eig_max[b]) * P.quality);
+    bool cand = false;
+    uint64_t key = 0;
+    if (x >= 1 && x < P.W - 1 && y >= 1 && y < P.H - 1) {
+        const float* e = P.eig + (int64_t)b * P.W * P.H;
+        float v = e[(int64_t)y * P.W + x];
+        v = v > thr ? v : 0.f;
+        if (v != 0.f) {
+            float m = v;
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    float u = e[(int64_t)(y + dy) * P.W + (x + dx)];
+                    u = u > thr ? u : 0.f;
+                    m = u > m ? u : m;
+                }
+            if (v == m) {
+                cand = true;
+                key = ((uint64_t)fkey(v) << 32) | (uint32_t)(y * P.W + x);
+            }
+        }
+    }
+    // wave-aggregated append (order is irrelevant: keys are unique and sorted later)
+    const unsigned long long m = __ballot(cand);
+    if (m == 0) return;
+    const int lane = lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&P.nkeys[b], __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (cand) {
+        const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (idx < P.ccap) P.keys[(int64_t)b * P.ccap + idx] = key;
+    }
+}
+
+// ---------------------------------------------------------------- GFTT selection
+#define SEL_THREADS 1024
+#define PAGE 4096
+#define ACC_MAX 8192
+#define GRID_LDS_CELLS 22528
+
+struct SelParams {
+    const uint64_t* keys;
+    const int32_t* nkeys;
+    int ccap, W, H;
+    int max_corners;
+    double min_dist;
+    float* corners;
+    int32_t* ncorners;
+    int mcap;
+    uint32_t* gscratch;      // per-chain L2 grid when the LDS grid is too small ([B][W*H] u32)
+    int64_t gstride;
+    int32_t* chain_status;
+};
+
+// A grid cell holds up to two accepted-corner indices (u16 each, 0xFFFF = empty); the
+// geometric bound (cell = round(minDistance) <= minDistance + 0.5) allows at most two.
+VO_DEV uint32_t cell_get(bool lds, uint32_t* lg, uint32_t* gg, int c)
+{
+    return lds ? lg[c] : atomicOr(&gg[c], 0u);   // atomics are L2-coherent
+}
+VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
+{
+    if (lds) lg[c] = v;
+    else atomicExch(&gg[c], v);
+}
+
+__global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
+{
+    __shared__ uint64_t page[PAGE];
+    __shared__ uint32_t lgrid[GRID_LDS_CELLS];
+    __shared__ uint32_t acc_xy[ACC_MAX];
+    __shared__ int hist[256];
+    __shared__ int sh_int[8];
+    __shared__ uint64_t sh_u64[4];
+    const int b = blockIdx.x;
+    if (P.chain_status[b] != 0) return;
+    const int tid = threadIdx.x;
+    const int nk = P.nkeys[b];
+    if (nk > P.ccap) {
+        if (tid == 0) P.chain_status[b] = VO_ST_CAPACITY;
+        return;
+    }
+    const uint64_t* keys = P.keys + (int64_t)b * P.ccap;
+    const double md = P.min_dist;
+    const bool use_grid = md >= 1;
+    const int cs = use_grid ? __double2int_rn(md) : 1;
+    const int gw = (P.W + cs - 1) / cs, gh = (P.H + cs - 1) / cs;
+    const double md2 = md * md;
+    const int want = P.max_corners > 0 ? P.max_corners : 0x7FFFFFFF;
+    const int cap = P.mcap < ACC_MAX ? P.mcap : ACC_MAX;
+    const int limit = want < cap ? want : cap;
+    const bool lds = (int64_t)gw * gh <= GRID_LDS_CELLS;
+    uint32_t* gg = P.gscratch + (int64_t)b * P.gstride;
+    if (use_grid) {
+        for (int q = tid; q < gw * gh; q += blockDim.x) cell_set(lds, lgrid, gg, q, 0xFFFFFFFFu);
+    }
+    float* out = P.corners + (int64_t)b * P.mcap * 2;
+    int nacc = 0;
+    bool has_upper = false;
+    uint64_t upper = 0;
+    int remaining = nk;
+    __syncthreads();
+    while (remaining > 0 && nacc < limit) {
+        // ---- this page: the min(PAGE, remaining) largest keys below `upper`
+        uint64_t thr = 0;
+        const int take = remaining < PAGE ? remaining : PAGE;
+        if (remaining > PAGE) {
+            uint64_t prefix = 0, mask = 0;
+            int k = PAGE;
+            for (int shift = 56; shift >= 0; shift -= 8) {
+                for (int q = tid; q < 256; q += blockDim.x) hist[q] = 0;
+                __syncthreads();
+                for (int i = tid; i < nk; i += blockDim.x) {
+                    const uint64_t kk = keys[i];
+                    if ((!has_upper || kk < upper) && (kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255], 1);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    int cum = 0, dsel = 0;
+                    for (int dgt = 255; dgt >= 0; --dgt) {
+                        if (cum + hist[dgt] >= k) { dsel = dgt; break; }
+                        cum += hist[dgt];
+                    }
+                    sh_u64[0] = prefix | ((uint64_t)dsel << shift);
+                    sh_int[0] = k - cum;
+                }
+                __syncthreads();
+                prefix = sh_u64[0];
+                k = sh_int[0];
+                mask |= (uint64_t)0xFF << shift;
+                __syncthreads();
+            }
+            thr = prefix;
+        }
+        if (tid == 0) sh_int[1] = 0;
+        __syncthreads();
+        for (int i = tid; i < nk; i += blockDim.x) {
+            const uint64_t kk = keys[i];
+            if ((!has_upper || kk < upper) && kk >= thr) {
+                const int pos = atomicAdd(&sh_int[1], 1);
+                if (pos < PAGE) page[pos] = kk;
+            }
+        }
+        __syncthreads();
+        for (int i = take + tid; i < PAGE; i += blockDim.x) page[i] = 0;
+        __syncthreads();
+        // ---- bitonic sort, descending (value desc, then larger address first)
+        for (int size = 2; size <= PAGE; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = tid; i < PAGE / 2; i += blockDim.x) {
+                    const int lo = 2 * i - (i & (stride - 1));
+                    const int hi = lo + stride;
+                    const bool desc = ((lo & size) == 0);
+                    const uint64_t a = page[lo], c = page[hi];
+                    if ((a < c) == desc) { page[lo] = c; page[hi] = a; }
+                }
+                __syncthreads();
+            }
+        }
+        // ---- greedy selection by wave 0, 64 candidates per round in sorted order
+        if (wave_id() == 0) {
+            const int lane = lane_id();
+            for (int s0 = 0; s0 < take && nacc < limit; s0 += 64) {
+                const int i = s0 + lane;
+                bool tent = i < take;
+                int x = 0, y = 0;
+                if (tent) {
+                    const uint32_t addr = (uint32_t)page[i];
+                    y = (int)(addr / (uint32_t)P.W);
+                    x = (int)(addr - (uint32_t)y * P.W);
+                }
+                const int xc = x / cs, yc = y / cs;
+                if (tent && use_grid) {
+                    const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
+                    const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
+                    for (int yy = y1; yy <= y2 && tent; ++yy)
+                        for (int xx = x1; xx <= x2 && tent; ++xx) {
+                            const uint32_t cv = cell_get(lds, lgrid, gg, yy * gw + xx);
+                            for (int q = 0; q < 2; ++q) {
+                                const uint32_t id = (cv >> (16 * q)) & 0xFFFFu;
+                                if (id == 0xFFFFu) break;
+                                const uint32_t a = acc_xy[id];
+                                const float ddx = (float)x - (float)(a & 0xFFFF);
+                                const float ddy = (float)y - (float)(a >> 16);
+                                if ((double)(ddx * ddx + ddy * ddy) < md2) { tent = false; break; }
+                            }
+                        }
+                }
+                while (true) {
+                    const unsigned long long m = __ballot(tent);
+                    if (m == 0 || nacc >= limit) break;
+                    const int t = __ffsll((long long)m) - 1;
+                    const int tx = __shfl(x, t, 64), ty = __shfl(y, t, 64);
+                    if (lane == t) {
+                        acc_xy[nacc] = (uint32_t)tx | ((uint32_t)ty << 16);
+                        out[2 * nacc] = (float)tx;
+                        out[2 * nacc + 1] = (float)ty;
+                        if (use_grid) {
+                            const int cell = (ty / cs) * gw + (tx / cs);
+                            const uint32_t cv = cell_get(lds, lgrid, gg, cell);
+                            uint32_t nv;
+                            if ((cv & 0xFFFFu) == 0xFFFFu) nv = (cv & 0xFFFF0000u) | (uint32_t)nacc;
+                            else nv = (cv & 0xFFFFu) | ((uint32_t)nacc << 16);
+                            cell_set(lds, lgrid, gg, cell, nv);
+                        }
+                        tent = false;
+                    }
+                    ++nacc;
+                    if (tent && use_grid && lane > t) {
+                        const int txc = tx / cs, tyc = ty / cs;
+                        if (abs(txc - xc) <= 1 && abs(tyc - yc) <= 1) {
+                            const float ddx = (float)x - (float)tx, ddy = (float)y - (float)ty;
+                            if ((double)(ddx * ddx + ddy * ddy) < md2) tent = false;
+                        }
+                    }
+                }
+            }
+            if (lane == 0) sh_int[2] = nacc;
+        }
+        __syncthreads();
+        nacc = sh_int[2];
+        upper = page[take - 1];
+        has_upper = true;
+        remaining -= take;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        P.ncorners[b] = nacc;
+        // more corners wanted than this engine can hold -> never truncate silently
+        if (nacc == cap && cap < want && remaining > 0) P.chain_status[b] = VO_ST_CAPACITY;
+    }
+}
+
+}  // namespace
+
+// ======================================================================= host side
+static inline bool hip_ok() { return hipGetLastError() == hipSuccess; }
+#define VO_STREAM(s) ((hipStream_t)(s))
+
+extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
+                            int64_t frame_stride, vo_stream_t stream)
+{
+    if (!d || !s || !frames || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
+    uint8_t* pyr = s->pyr[cur];
+    {
+        const int pw = d->W + 2 * VO_BORDER, ph = d->H + 2 * VO_BORDER;
+        dim3 g((pw + 255) / 256, ph, d->B);
+        hipLaunchKernelGGL(k_ingest, g, dim3(256), 0, VO_STREAM(stream), frames, frame_stride, pyr, d->pyr_stride,
+                           d->W, d->H, d->lvl_pitch[0], d->lvl_off[0]);
+    }
+    for (int l = 1; l < d->nlev; ++l) {
+        const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
+        dim3 g((pw + 255) / 256, ph, d->B);
+        hipLaunchKernelGGL(k_pyrdown, g, dim3(256), 0, VO_STREAM(stream), pyr, d->pyr_stride, d->lvl_w[l - 1],
+                           d->lvl_pitch[l - 1], d->lvl_off[l - 1], d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l],
+                           d->lvl_off[l]);
+    }
+    return hip_ok() ? VO_OK : VO_EHIP;
+}
+
+extern "C" int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t stream)
+{
+    if (!d || !s || which < 0 || which > 1) return VO_EARG;
+    for (int l = 0; l < d->nlev; ++l) {
+        const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
+        dim3 g((pw + 255) / 256, ph, d->B);
+        hipLaunchKernelGGL(k_scharr, g, dim3(256), 0, VO_STREAM(stream), s->pyr[which], d->pyr_stride, s->der,
+                           d->der_stride, d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l], d->lvl_off[l]);
+    }
+    return hip_ok() ? VO_OK : VO_EHIP;
+}
+
+static void fill_lk(LKParams& P, const vo_dims* d, const vo_opts* o, const vo_state* s, int prev)
+{
+    P.prev = s->pyr[prev];
+    P.next = s->pyr[1 - prev];
+    P.der = s->der;
+    P.pstride = d->pyr_stride;
+    P.dstride = d->der_stride;
+    P.L = d->nlev - 1;
+    for (int l = 0; l < VO_MAX_LEVELS; ++l) {
+        P.lw[l] = d->lvl_w[l];
+        P.lh[l] = d->lvl_h[l];
+        P.lpitch[l] = d->lvl_pitch[l];
+        P.loff[l] = d->lvl_off[l];
+    }
+    P.win_w = o->win_w;
+    P.win_h = o->win_h;
+    int mc = o->crit_count;
+    double eps = o->crit_eps;
+    if (!(o->crit_type & 1)) mc = 30;
+    else mc = mc < 0 ? 0 : (mc > 100 ? 100 : mc);
+    if (!(o->crit_type & 2)) eps = 0.01;
+    else eps = eps < 0 ? 0 : (eps > 10 ? 10 : eps);
+    P.max_count = mc;
+    P.eps2 = eps * eps;
+    P.min_eig = (float)o->min_eig;
+}
+
+static int launch_lk(const LKParams& P, int B, hipStream_t st)
+{
+    const int npx = P.win_w * P.win_h;
+    if (P.win_w <= 2 || P.win_h <= 2 || npx > 64 * 16) return VO_EARG;
+    dim3 g(64, B);
+    if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, g, dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(k_lk<16>, g, dim3(256), 0, st, P);
+    return hip_ok() ? VO_OK : VO_EHIP;
+}
+
+extern "C" int vo_track(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, vo_stream_t stream)
+{
+    if (!d || !o || !s || prev < 0 || prev > 1) return VO_EARG;
+    LKParams P;
+    fill_lk(P, d, o, s, prev);
+    P.p0 = s->lm_kp; P.n0 = s->nL; P.cap0 = d->ncap;
+    P.p1 = s->c_kp; P.n1 = s->nC; P.cap1 = d->pcap; P.seg1_min = 1;   // :286 "if P > 1"
+    P.chain_status = s->status;
+    P.out = s->trk_pts; P.st = s->trk_st; P.err = s->trk_err; P.ocap = d->ncap + d->pcap;
+    int rc = launch_lk(P, d->B, VO_STREAM(stream));
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_track_compact, dim3(d->B), dim3(256), 0, VO_STREAM(stream), *d, *s);
+    return hip_ok() ? VO_OK : VO_EHIP;
+}
+
+extern "C" int vo_lk_points(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, const float* pts,
+                            const int32_t* counts, int32_t cap, float* out_pts, uint8_t* out_status, float* out_err,
+                            vo_stream_t stream)
+{
+    if (!d || !o || !s || !pts || !counts || !out_pts || !out_status) return VO_EARG;
+    LKParams P;
+    fill_lk(P, d, o, s, prev);
+    P.p0 = pts; P.n0 = counts; P.cap0 = cap;
+    P.p1 = nullptr; P.n1 = nullptr; P.cap1 = 0; P.seg1_min = 0;
+    P.chain_status = nullptr;
+    P.out = out_pts; P.st = out_status; P.err = out_err; P.ocap = cap;
+    return launch_lk(P, d->B, VO_STREAM(stream));
+}
+
+extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream)
+{
+    if (!d || !o || !s || cur < 0 || cur > 1) return VO_EARG;
+    if (o->feature_block_size < 1 || o->feature_block_size > EIG_MAXBS) return VO_EARG;
+    hipStream_t st = VO_STREAM(stream);
+    if (hipMemsetAsync(s->eig_max, 0, sizeof(uint32_t) * d->B, st) != hipSuccess) return VO_EHIP;
+    if (hipMemsetAsync(s->gf_n, 0, sizeof(int32_t) * d->B, st) != hipSuccess) return VO_EHIP;
+    EigParams E;
+    E.pyr = s->pyr[cur]; E.pstride = d->pyr_stride; E.W = d->W; E.H = d->H; E.pitch = d->lvl_pitch[0];
+    E.off = d->lvl_off[0]; E.bs = o->feature_block_size; E.harris = o->feature_use_harris; E.harris_k = o->harris_k;
+    E.eig = s->eig; E.eig_max = s->eig_max; E.chain_status = s->status;
+    dim3 g((d->W + EIG_T - 1) / EIG_T, (d->H + EIG_T - 1) / EIG_T, d->B);
+    hipLaunchKernelGGL(k_eig, g, dim3(256), 0, st, E);
+    NmsParams N;
+    N.eig = s->eig; N.eig_max = s->eig_max; N.W = d->W; N.H = d->H; N.quality = o->feature_quality_level;
+    N.keys = s->gf_keys; N.nkeys = s->gf_n; N.ccap = d->ccap; N.chain_status = s->status;
+    hipLaunchKernelGGL(k_nms, g, dim3(256), 0, st, N);
+    SelParams S;
+    S.keys = s->gf_keys; S.nkeys = s->gf_n; S.ccap = d->ccap; S.W = d->W; S.H = d->H;
+    S.max_corners = o->feature_max_corners; S.min_dist = o->feature_min_dist;
+    S.corners = s->corners; S.ncorners = s->nCorners; S.mcap = d->mcap; S.chain_status = s->status;
+    S.gscratch = (uint32_t*)s->eig;      // the eigen map is dead after NMS: reuse it as L2 grid
+    S.gstride = (int64_t)d->W * d->H;
+    hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), 0, st, S);
+    return hip_ok() ? VO_OK : VO_EHIP;
+}

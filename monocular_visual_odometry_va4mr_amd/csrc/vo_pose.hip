@@ -1,0 +1,916 @@
+// Pose-side kernels for gfx950: PnP-RANSAC (P3P hypotheses, wave-parallel scoring,
+// OpenCV's sequential "first strictly better + adaptive niters" rule) with the EPnP
+// refit, candidate triangulation with ordered append/compaction, and the feature-adding
+// distance filter + step finish.
+//
+// Reference call sites: VisualOdometryPipeLine.py:107-206 (triangulate_landmarks incl.
+// cv2.triangulatePoints :188), :248-268 (feature_adding filter), :338-373 (PnP step and
+// bookkeeping).  fp64 geometry lives in vo_dgeom.h and mirrors oracle/vo_oracle_geom.c.
+#include "vo_dgeom.h"
+
+namespace {
+
+using namespace vg;
+
+// ------------------------------------------------------------------ EPnP (block)
+struct EpnpShared {
+    double cws[4][3], ccs[4][3];
+    double CCi[9];
+    double V12[144];
+    double L[60], rho[6];
+    double betas[4][4], rep[4], Rs[4][9], ts[4][3];
+    double tmp[80];
+    double pc0[3], pw0[3];
+    int flip;
+};
+
+// Sum over n items of K-vectors in the oracle's fixed order (lane = item % 64, then a
+// shuffle tree 32..1).  Executed by wave 0; result in out[0..K) (LDS).
+template <int K, class F>
+VO_DEV void wave_det_sum(int n, F f, double* out)
+{
+    const int lane = lane_id();
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        double c[K];
+        f(i, c);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] += c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double v = acc[k];
+        for (int s = 32; s >= 1; s >>= 1) v += __shfl_down(v, s, 64);
+        if (lane == 0) out[k] = v;
+    }
+}
+
+VO_DEV void qr_lsq(double* A, int m, int n, double* b, double* x)
+{
+    for (int k = 0; k < n; ++k) {
+        double nrm = 0;
+        for (int i = k; i < m; ++i) nrm += A[i * n + k] * A[i * n + k];
+        nrm = sqrt(nrm);
+        if (nrm == 0) continue;
+        double alpha = A[k * n + k] > 0 ? -nrm : nrm;
+        double v[16];
+        for (int i = k; i < m; ++i) v[i] = A[i * n + k];
+        v[k] -= alpha;
+        double vn = 0;
+        for (int i = k; i < m; ++i) vn += v[i] * v[i];
+        if (vn == 0) continue;
+        for (int j = k; j < n; ++j) {
+            double s = 0;
+            for (int i = k; i < m; ++i) s += v[i] * A[i * n + j];
+            s = 2.0 * s / vn;
+            for (int i = k; i < m; ++i) A[i * n + j] -= s * v[i];
+        }
+        double s = 0;
+        for (int i = k; i < m; ++i) s += v[i] * b[i];
+        s = 2.0 * s / vn;
+        for (int i = k; i < m; ++i) b[i] -= s * v[i];
+    }
+    for (int k = n - 1; k >= 0; --k) {
+        double s = b[k];
+        for (int j = k + 1; j < n; ++j) s -= A[k * n + j] * x[j];
+        x[k] = (A[k * n + k] != 0) ? s / A[k * n + k] : 0.0;
+    }
+}
+
+VO_DEV void epnp_gauss_newton(const double* L, const double* rho, double* betas)
+{
+    for (int it = 0; it < 5; ++it) {
+        double A[24], b[6], x[4];
+        for (int i = 0; i < 6; ++i) {
+            const double* rL = L + i * 10;
+            double* rA = A + i * 4;
+            rA[0] = 2 * rL[0] * betas[0] + rL[1] * betas[1] + rL[3] * betas[2] + rL[6] * betas[3];
+            rA[1] = rL[1] * betas[0] + 2 * rL[2] * betas[1] + rL[4] * betas[2] + rL[7] * betas[3];
+            rA[2] = rL[3] * betas[0] + rL[4] * betas[1] + 2 * rL[5] * betas[2] + rL[8] * betas[3];
+            rA[3] = rL[6] * betas[0] + rL[7] * betas[1] + rL[8] * betas[2] + 2 * rL[9] * betas[3];
+            b[i] = rho[i] - (rL[0] * betas[0] * betas[0] + rL[1] * betas[0] * betas[1] +
+                             rL[2] * betas[1] * betas[1] + rL[3] * betas[0] * betas[2] +
+                             rL[4] * betas[1] * betas[2] + rL[5] * betas[2] * betas[2] +
+                             rL[6] * betas[0] * betas[3] + rL[7] * betas[1] * betas[3] +
+                             rL[8] * betas[2] * betas[3] + rL[9] * betas[3] * betas[3]);
+        }
+        qr_lsq(A, 6, 4, b, x);
+        for (int i = 0; i < 4; ++i) betas[i] += x[i];
+    }
+}
+
+__constant__ int PAIR_A[6] = {0, 0, 0, 1, 1, 2};
+__constant__ int PAIR_B[6] = {1, 2, 3, 2, 3, 3};
+
+VO_DEV void epnp_L6x10(const double* V12, double* L)
+{
+    double dv[4][6][3];
+    for (int i = 0; i < 4; ++i) {
+        int col = 11 - i;
+        for (int j = 0; j < 6; ++j) {
+            int a = PAIR_A[j], b = PAIR_B[j];
+            for (int k = 0; k < 3; ++k) dv[i][j][k] = V12[(3 * a + k) * 12 + col] - V12[(3 * b + k) * 12 + col];
+        }
+    }
+#define DOT3(p, q) ((p)[0] * (q)[0] + (p)[1] * (q)[1] + (p)[2] * (q)[2])
+    for (int i = 0; i < 6; ++i) {
+        double* row = L + 10 * i;
+        row[0] = DOT3(dv[0][i], dv[0][i]);
+        row[1] = 2.0 * DOT3(dv[0][i], dv[1][i]);
+        row[2] = DOT3(dv[1][i], dv[1][i]);
+        row[3] = 2.0 * DOT3(dv[0][i], dv[2][i]);
+        row[4] = 2.0 * DOT3(dv[1][i], dv[2][i]);
+        row[5] = DOT3(dv[2][i], dv[2][i]);
+        row[6] = 2.0 * DOT3(dv[0][i], dv[3][i]);
+        row[7] = 2.0 * DOT3(dv[1][i], dv[3][i]);
+        row[8] = 2.0 * DOT3(dv[2][i], dv[3][i]);
+        row[9] = DOT3(dv[3][i], dv[3][i]);
+    }
+#undef DOT3
+}
+
+// compute_R_and_t for approximation `a` (all threads participate)
+VO_DEV void epnp_R_and_t(EpnpShared& S, int a, const double* K, const double* pws, const double* us,
+                         const double* alphas, double* pcs, int n)
+{
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        for (int j = 0; j < 4; ++j) for (int k = 0; k < 3; ++k) S.ccs[j][k] = 0;
+        for (int i = 0; i < 4; ++i) {
+            int col = 11 - i;
+            for (int j = 0; j < 4; ++j)
+                for (int k = 0; k < 3; ++k) S.ccs[j][k] += S.betas[a][i] * S.V12[(3 * j + k) * 12 + col];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+        const double* al = alphas + 4 * i;
+        for (int j = 0; j < 3; ++j)
+            pcs[3 * i + j] = al[0] * S.ccs[0][j] + al[1] * S.ccs[1][j] + al[2] * S.ccs[2][j] + al[3] * S.ccs[3][j];
+    }
+    __syncthreads();
+    if (tid == 0) S.flip = pcs[2] < 0.0;
+    __syncthreads();
+    if (S.flip) {
+        if (tid == 0) for (int j = 0; j < 4; ++j) for (int k = 0; k < 3; ++k) S.ccs[j][k] = -S.ccs[j][k];
+        for (int i = tid; i < 3 * n; i += blockDim.x) pcs[i] = -pcs[i];
+    }
+    __syncthreads();
+    if (wave_id() == 0) {
+        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pcs[3 * i]; c[1] = pcs[3 * i + 1]; c[2] = pcs[3 * i + 2]; }, S.tmp);
+    }
+    __syncthreads();
+    if (tid == 0) for (int j = 0; j < 3; ++j) S.pc0[j] = S.tmp[j] / n;
+    __syncthreads();
+    if (wave_id() == 0) {
+        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp);
+    }
+    __syncthreads();
+    if (tid == 0) for (int j = 0; j < 3; ++j) S.pw0[j] = S.tmp[j] / n;
+    __syncthreads();
+    if (wave_id() == 0) {
+        wave_det_sum<9>(n, [&](int i, double* c) {
+            for (int j = 0; j < 3; ++j)
+                for (int k = 0; k < 3; ++k) c[j * 3 + k] = (pcs[3 * i + j] - S.pc0[j]) * (pws[3 * i + k] - S.pw0[k]);
+        }, S.tmp);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double abt[9], w[3], V[9];
+        for (int q = 0; q < 9; ++q) abt[q] = S.tmp[q];
+        svd_jacobi<3, 3>(abt, w, V);
+        double* R = S.Rs[a];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                R[i * 3 + j] = abt[i * 3 + 0] * V[j * 3 + 0] + abt[i * 3 + 1] * V[j * 3 + 1] + abt[i * 3 + 2] * V[j * 3 + 2];
+        if (det3(R) < 0) { R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8]; }
+        for (int i = 0; i < 3; ++i)
+            S.ts[a][i] = S.pc0[i] - (R[i * 3] * S.pw0[0] + R[i * 3 + 1] * S.pw0[1] + R[i * 3 + 2] * S.pw0[2]);
+    }
+    __syncthreads();
+    if (wave_id() == 0) {
+        const double* R = S.Rs[a];
+        const double* t = S.ts[a];
+        const double fu = K[0], fv = K[4], uc = K[2], vc = K[5];
+        wave_det_sum<1>(n, [&](int i, double* c) {
+            const double* pw = pws + 3 * i;
+            double Xc = R[0] * pw[0] + R[1] * pw[1] + R[2] * pw[2] + t[0];
+            double Yc = R[3] * pw[0] + R[4] * pw[1] + R[5] * pw[2] + t[1];
+            double inv_Zc = 1.0 / (R[6] * pw[0] + R[7] * pw[1] + R[8] * pw[2] + t[2]);
+            double ue = uc + fu * Xc * inv_Zc;
+            double ve = vc + fv * Yc * inv_Zc;
+            double u = us[2 * i], v = us[2 * i + 1];
+            c[0] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+        }, S.tmp);
+    }
+    __syncthreads();
+    if (tid == 0) S.rep[a] = S.tmp[0] / n;
+    __syncthreads();
+}
+
+// EPnP (epnp::compute_pose), all threads of the block; n >= 4
+VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const double* us, double* alphas,
+                       double* pcs, int n, double* Rout, double* tout)
+{
+    const int tid = threadIdx.x;
+    if (wave_id() == 0)
+        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp);
+    __syncthreads();
+    if (tid == 0) for (int j = 0; j < 3; ++j) S.cws[0][j] = S.tmp[j] / n;
+    __syncthreads();
+    if (wave_id() == 0)
+        wave_det_sum<9>(n, [&](int i, double* c) {
+            double d[3];
+            for (int j = 0; j < 3; ++j) d[j] = pws[3 * i + j] - S.cws[0][j];
+            for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) c[a * 3 + b] = d[a] * d[b];
+        }, S.tmp);
+    __syncthreads();
+    if (tid == 0) {
+        double cov[9], dc[3], Vc[9];
+        for (int q = 0; q < 9; ++q) cov[q] = S.tmp[q];
+        svd_jacobi<3, 3>(cov, dc, Vc);
+        for (int i = 1; i < 4; ++i) {
+            double k = sqrt(dc[i - 1] / n);
+            for (int j = 0; j < 3; ++j) S.cws[i][j] = S.cws[0][j] + k * cov[j * 3 + (i - 1)];
+        }
+        double CC[9], w[3], V[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 1; j < 4; ++j) CC[3 * i + j - 1] = S.cws[j][i] - S.cws[0][i];
+        svd_jacobi<3, 3>(CC, w, V);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                double s = 0;
+                for (int k = 0; k < 3; ++k) if (w[k] > DBL_EPSILON * w[0] * 3) s += V[i * 3 + k] * CC[j * 3 + k] / w[k];
+                S.CCi[i * 3 + j] = s;
+            }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += blockDim.x) {
+        const double* pi = pws + 3 * i;
+        double* a = alphas + 4 * i;
+        for (int j = 0; j < 3; ++j)
+            a[1 + j] = S.CCi[3 * j] * (pi[0] - S.cws[0][0]) + S.CCi[3 * j + 1] * (pi[1] - S.cws[0][1]) +
+                       S.CCi[3 * j + 2] * (pi[2] - S.cws[0][2]);
+        a[0] = 1.0 - a[1] - a[2] - a[3];
+    }
+    __syncthreads();
+    // M^T M upper triangle (78 entries), 6 groups of 13
+    const double fu = K[0], fv = K[4], uc = K[2], vc = K[5];
+    __shared__ double up[78];
+    for (int g = 0; g < 6; ++g) {
+        if (wave_id() == 0) {
+            wave_det_sum<13>(n, [&](int i, double* c) {
+                double M1[12], M2[12];
+                const double* as = alphas + 4 * i;
+                double u = us[2 * i], v = us[2 * i + 1];
+                for (int k = 0; k < 4; ++k) {
+                    M1[3 * k] = as[k] * fu; M1[3 * k + 1] = 0.0; M1[3 * k + 2] = as[k] * (uc - u);
+                    M2[3 * k] = 0.0; M2[3 * k + 1] = as[k] * fv; M2[3 * k + 2] = as[k] * (vc - v);
+                }
+                int q = 0;
+                for (int a = 0; a < 12; ++a)
+                    for (int b = a; b < 12; ++b, ++q)
+                        if (q >= 13 * g && q < 13 * g + 13) c[q - 13 * g] = M1[a] * M1[b] + M2[a] * M2[b];
+            }, up + 13 * g);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double MtM[144], dM[12];
+        int q = 0;
+        for (int a = 0; a < 12; ++a) for (int b = a; b < 12; ++b) { MtM[a * 12 + b] = MtM[b * 12 + a] = up[q++]; }
+        svd_jacobi<12, 12>(MtM, dM, S.V12);
+        epnp_L6x10(S.V12, S.L);
+        for (int j = 0; j < 6; ++j) {
+            const double* p = S.cws[PAIR_A[j]];
+            const double* r = S.cws[PAIR_B[j]];
+            S.rho[j] = (p[0] - r[0]) * (p[0] - r[0]) + (p[1] - r[1]) * (p[1] - r[1]) + (p[2] - r[2]) * (p[2] - r[2]);
+        }
+        {
+            double A[24], b4[4];
+            const int cols[4] = {0, 1, 3, 6};
+            for (int i = 0; i < 6; ++i) for (int j = 0; j < 4; ++j) A[i * 4 + j] = S.L[i * 10 + cols[j]];
+            lsq_svd<6, 4>(A, S.rho, b4);
+            double* B = S.betas[1];
+            if (b4[0] < 0) { B[0] = sqrt(-b4[0]); B[1] = -b4[1] / B[0]; B[2] = -b4[2] / B[0]; B[3] = -b4[3] / B[0]; }
+            else { B[0] = sqrt(b4[0]); B[1] = b4[1] / B[0]; B[2] = b4[2] / B[0]; B[3] = b4[3] / B[0]; }
+            epnp_gauss_newton(S.L, S.rho, B);
+        }
+        {
+            double A[18], b3[3];
+            for (int i = 0; i < 6; ++i) for (int j = 0; j < 3; ++j) A[i * 3 + j] = S.L[i * 10 + j];
+            lsq_svd<6, 3>(A, S.rho, b3);
+            double* B = S.betas[2];
+            if (b3[0] < 0) { B[0] = sqrt(-b3[0]); B[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0; }
+            else { B[0] = sqrt(b3[0]); B[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0; }
+            if (b3[1] < 0) B[0] = -B[0];
+            B[2] = 0.0; B[3] = 0.0;
+            epnp_gauss_newton(S.L, S.rho, B);
+        }
+        {
+            double A[30], b5[5];
+            for (int i = 0; i < 6; ++i) for (int j = 0; j < 5; ++j) A[i * 5 + j] = S.L[i * 10 + j];
+            lsq_svd<6, 5>(A, S.rho, b5);
+            double* B = S.betas[3];
+            if (b5[0] < 0) { B[0] = sqrt(-b5[0]); B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0; }
+            else { B[0] = sqrt(b5[0]); B[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0; }
+            if (b5[1] < 0) B[0] = -B[0];
+            B[2] = b5[3] / B[0]; B[3] = 0.0;
+            epnp_gauss_newton(S.L, S.rho, B);
+        }
+    }
+    __syncthreads();
+    // the oracle runs approximation 1's R,t before computing approximation 2's betas; the
+    // betas do not depend on R,t, so computing all betas first is equivalent
+    for (int a = 1; a <= 3; ++a) epnp_R_and_t(S, a, K, pws, us, alphas, pcs, n);
+    if (tid == 0) {
+        int N = 1;
+        if (S.rep[2] < S.rep[1]) N = 2;
+        if (S.rep[3] < S.rep[N]) N = 3;
+        for (int q = 0; q < 9; ++q) Rout[q] = S.Rs[N][q];
+        for (int q = 0; q < 3; ++q) tout[q] = S.ts[N][q];
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------ PnP-RANSAC
+#define HYP 64
+
+struct PnPArgs {
+    double K[9];
+    float thr;              // (float)(reprojectionError^2)
+    double conf;
+    int iters;
+    int min_points;
+    const float* obj;       // [B][cap][3]
+    const float* img;       // [B][cap][2]
+    const int32_t* counts;
+    int cap;
+    const int32_t* chain_status;
+    double* work;           // [B][work_stride]
+    int64_t work_stride;
+    int32_t* iwork;         // [B][iwork_stride]
+    int64_t iwork_stride;
+    // outputs (may alias iwork/work for the engine)
+    double* rvec;           // [B][3]
+    double* tvec;           // [B][3]
+    int32_t* success;       // [B]
+    uint8_t* mask;          // [B][cap]
+    int32_t* n_inl;         // [B]
+};
+
+__global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
+{
+    __shared__ int sub[HYP][4];
+    __shared__ double mdl[HYP][12];
+    __shared__ int valid[HYP], cnt[HYP];
+    __shared__ double bestm[12];
+    __shared__ int sh[8];
+    __shared__ int lds16[16];
+    __shared__ EpnpShared S;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (A.chain_status && A.chain_status[b] != 0) return;
+    const int n = A.counts[b];
+    const float* obj = A.obj + (int64_t)b * A.cap * 3;
+    const float* img = A.img + (int64_t)b * A.cap * 2;
+    uint8_t* mask = A.mask + (int64_t)b * A.cap;
+    if (n < 4 || n < A.min_points) {
+        if (tid == 0) { A.success[b] = 0; A.n_inl[b] = 0; }
+        return;
+    }
+    const CamK k = camk(A.K);
+    if (n == 4) {
+        if (tid == 0) {
+            double o[12], im[8], R[9], t[3];
+            for (int i = 0; i < 12; ++i) o[i] = obj[i];
+            for (int i = 0; i < 8; ++i) im[i] = img[i];
+            int ok = p3p_solve4(k, o, im, R, t);
+            A.success[b] = ok;
+            A.n_inl[b] = ok ? 4 : 0;
+            if (ok) {
+                rodrigues_m2v(R, A.rvec + 3 * b);
+                for (int q = 0; q < 3; ++q) A.tvec[3 * b + q] = t[q];
+            }
+            for (int i = 0; i < 4; ++i) mask[i] = ok ? 1 : 0;
+        }
+        return;
+    }
+    uint64_t rng = ~0ULL;   // only thread 0's copy is used
+    if (tid == 0) { sh[0] = 0; sh[1] = A.iters > 1 ? A.iters : 1; sh[2] = 0; }
+    __syncthreads();
+    while (true) {
+        const int it0 = sh[0];
+        const int niters0 = sh[1];
+        if (it0 >= niters0) break;
+        if (tid == 0) {
+            for (int h = 0; h < HYP; ++h) {
+                for (int i = 0; i < 4; ++i) {
+                    for (;;) {
+                        int v = (int)(rng_next(rng) % (uint32_t)n);
+                        int j;
+                        for (j = 0; j < i; ++j) if (v == sub[h][j]) break;
+                        sub[h][i] = v;
+                        if (j == i) break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < HYP) {
+            const int h = tid;
+            double o[12], im[8], R[9], t[3];
+            for (int j = 0; j < 4; ++j) {
+                const int id = sub[h][j];
+                o[3 * j] = obj[3 * id]; o[3 * j + 1] = obj[3 * id + 1]; o[3 * j + 2] = obj[3 * id + 2];
+                im[2 * j] = img[2 * id]; im[2 * j + 1] = img[2 * id + 1];
+            }
+            const int ok = (it0 + h < niters0) ? p3p_solve4(k, o, im, R, t) : 0;
+            valid[h] = ok;
+            if (ok) {
+                for (int q = 0; q < 9; ++q) mdl[h][q] = R[q];
+                for (int q = 0; q < 3; ++q) mdl[h][9 + q] = t[q];
+            }
+        }
+        __syncthreads();
+        {
+            const int w = wave_id(), lane = lane_id();
+            const int hpw = HYP / (blockDim.x >> 6);
+            for (int h = w * hpw; h < (w + 1) * hpw; ++h) {
+                if (!valid[h]) { if (lane == 0) cnt[h] = 0; continue; }
+                const double* R = mdl[h];
+                const double* t = mdl[h] + 9;
+                int c = 0;
+                for (int i = lane; i < n; i += 64)
+                    c += pnp_err(R, t, k, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= A.thr;
+                c = wave_sum_i32(c);
+                if (lane == 0) cnt[h] = c;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int niters = sh[1], best = sh[2];
+            for (int h = 0; h < HYP; ++h) {
+                if (it0 + h >= niters) break;
+                if (!valid[h]) continue;
+                const int good = cnt[h];
+                if (good > (best > 3 ? best : 3)) {
+                    best = good;
+                    for (int q = 0; q < 12; ++q) bestm[q] = mdl[h][q];
+                    niters = ransac_update_niters(A.conf, (double)(n - good) / n, 4, niters);
+                }
+            }
+            sh[0] = it0 + HYP;
+            sh[1] = niters;
+            sh[2] = best;
+        }
+        __syncthreads();
+    }
+    if (sh[2] <= 0) {
+        if (tid == 0) { A.success[b] = 0; A.n_inl[b] = 0; }
+        for (int i = tid; i < n; i += blockDim.x) mask[i] = 0;
+        return;
+    }
+    // inlier mask of the best model + ordered compaction into fp64 scratch
+    double* work = A.work + (int64_t)b * A.work_stride;
+    double* pws = work;                       // [n][3]
+    double* us = work + 3 * A.cap;            // [n][2]
+    double* alphas = work + 5 * A.cap;        // [n][4]
+    double* pcs = work + 9 * A.cap;           // [n][3]
+    int m = 0;
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + tid;
+        bool in = false;
+        if (i < n) {
+            in = pnp_err(bestm, bestm + 9, k, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= A.thr;
+            mask[i] = in ? 1 : 0;
+        }
+        int tot;
+        const int pos = m + block_scan_flag(in, lds16, &tot);
+        if (in) {
+            pws[3 * pos] = obj[3 * i]; pws[3 * pos + 1] = obj[3 * i + 1]; pws[3 * pos + 2] = obj[3 * i + 2];
+            const double un = ((double)img[2 * i] - k.cx) * k.ifx, vn = ((double)img[2 * i + 1] - k.cy) * k.ify;
+            us[2 * pos] = un * k.fx + k.cx;
+            us[2 * pos + 1] = vn * k.fy + k.cy;
+        }
+        m += tot;
+    }
+    __syncthreads();
+    __shared__ double Rfin[9], tfin[3];
+    epnp_block(S, A.K, pws, us, alphas, pcs, m, Rfin, tfin);
+    if (tid == 0) {
+        rodrigues_m2v(Rfin, A.rvec + 3 * b);
+        for (int q = 0; q < 3; ++q) A.tvec[3 * b + q] = tfin[q];
+        A.success[b] = 1;
+        A.n_inl[b] = m;
+    }
+}
+
+// engine epilogue of the PnP step (:342-358): guard, inlier filtering, Rodrigues, inversion
+__global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const double* rvec, const double* tvec,
+                                                   const int32_t* success, const uint8_t* mask_all)
+{
+    __shared__ int lds[16];
+    __shared__ double Rwc[9];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (s.status[b] != 0) return;
+    const int n = s.nL[b];
+    if (n < 8) { if (tid == 0) s.status[b] = VO_ST_NOT_ENOUGH_KP; return; }
+    if (!success[b]) { if (tid == 0) s.status[b] = VO_ST_PNP_FAILED; return; }
+    const uint8_t* mask = mask_all + (int64_t)b * d.ncap;
+    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    const int kcap = d.ncap > d.pcap ? d.ncap : d.pcap;
+    float* outl = s.outl_kp + (int64_t)b * kcap * 2;
+    float* inl = s.inl_kp + (int64_t)b * kcap * 2;
+    int nin = 0, nout = 0;
+    for (int base = 0; base < n; base += blockDim.x) {
+        const int i = base + tid;
+        const bool valid = i < n;
+        const bool in = valid && mask[i];
+        float x0 = 0, x1 = 0, x2 = 0, k0 = 0, k1 = 0;
+        if (valid) { x0 = X[3 * i]; x1 = X[3 * i + 1]; x2 = X[3 * i + 2]; k0 = kp[2 * i]; k1 = kp[2 * i + 1]; }
+        int tin, tout;
+        const int pin = nin + block_scan_flag(in, lds, &tin);
+        const int pout = nout + block_scan_flag(valid && !in, lds, &tout);
+        if (in) {
+            X[3 * pin] = x0; X[3 * pin + 1] = x1; X[3 * pin + 2] = x2;
+            kp[2 * pin] = k0; kp[2 * pin + 1] = k1;
+            inl[2 * pin] = k0; inl[2 * pin + 1] = k1;
+        } else if (valid) {
+            outl[2 * pout] = k0; outl[2 * pout + 1] = k1;
+        }
+        nin += tin;
+        nout += tout;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        s.nL[b] = nin;
+        s.nInl[b] = nin;
+        s.nOutl[b] = nout;
+        rodrigues_v2m(rvec + 3 * b, Rwc);
+        const int f = s.nF[b];
+        if (f >= d.fcap) { s.status[b] = VO_ST_CAPACITY; return; }
+        double* Rcw = s.pose_R + ((int64_t)b * d.fcap + f) * 9;
+        double* tcw = s.pose_t + ((int64_t)b * d.fcap + f) * 3;
+        const double* t = tvec + 3 * b;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Rcw[i * 3 + j] = Rwc[j * 3 + i];
+        for (int i = 0; i < 3; ++i) tcw[i] = -(Rcw[i * 3] * t[0] + Rcw[i * 3 + 1] * t[1] + Rcw[i * 3 + 2] * t[2]);
+    }
+}
+
+// ------------------------------------------------------------------ triangulation
+struct TriArgs {
+    vo_dims d;
+    vo_state s;
+    double K[9], Kinv[9];
+    double min_d, max_d, min_angle;
+    int min_frames;
+    int force;
+};
+
+__global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
+{
+    __shared__ int lds[16];
+    __shared__ double Rc[9], tc[3], Rcwc[9], tcwc[3], Pc[12];
+    __shared__ int sh_fail;
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    if (s.status[b] != 0) return;
+    const int nC = s.nC[b];
+    if (!A.force && nC <= 1) return;                                  // :366
+    const int nF = s.nF[b];
+    const double* poseR = s.pose_R + (int64_t)b * d.fcap * 9;
+    const double* poset = s.pose_t + (int64_t)b * d.fcap * 3;
+    if (tid == 0) {
+        sh_fail = 0;
+        // current pose (R_CW, t_CW) is slot nF; (R_WC, t_WC) = (R^T, -R^T t)
+        for (int i = 0; i < 9; ++i) Rc[i] = poseR[(int64_t)nF * 9 + i];
+        for (int i = 0; i < 3; ++i) tc[i] = poset[(int64_t)nF * 3 + i];
+        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rcwc[i * 3 + j] = Rc[j * 3 + i];
+        for (int i = 0; i < 3; ++i) tcwc[i] = -(Rcwc[i * 3] * tc[0] + Rcwc[i * 3 + 1] * tc[1] + Rcwc[i * 3 + 2] * tc[2]);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 4; ++j) {
+                double acc = 0;
+                for (int q = 0; q < 3; ++q) acc += A.K[i * 3 + q] * (j < 3 ? Rcwc[q * 3 + j] : tcwc[q]);
+                Pc[i * 4 + j] = acc;
+            }
+    }
+    __syncthreads();
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    int nL = s.nL[b];
+    int kept = 0;
+    for (int base = 0; base < nC; base += blockDim.x) {
+        const int i = base + tid;
+        bool retain = false, accept = false;
+        float k0 = 0, k1 = 0, f0 = 0, f1 = 0, Xo[3] = {0, 0, 0};
+        int tau = 0;
+        if (i < nC) {
+            k0 = ck[2 * i]; k1 = ck[2 * i + 1]; f0 = cf[2 * i]; f1 = cf[2 * i + 1]; tau = ct[i];
+            if (nF > 1 && nF - tau <= A.min_frames) {
+                retain = true;                                        // :175-178
+            } else {
+                const double* Rp = poseR + (int64_t)tau * 9;
+                const double* tp = poset + (int64_t)tau * 3;
+                // check_baseline :117-147: v_cur = K^-1 [u;1], v_past = ((R_cur^T R_past)^T K^-1) [u_f;1]
+                double vc[3], vp[3], rel[9], Mr[9];
+                for (int r = 0; r < 3; ++r) vc[r] = A.Kinv[r * 3] * (double)k0 + A.Kinv[r * 3 + 1] * (double)k1 + A.Kinv[r * 3 + 2];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        rel[c * 3 + r] = Rc[0 * 3 + r] * Rp[0 * 3 + c] + Rc[1 * 3 + r] * Rp[1 * 3 + c] + Rc[2 * 3 + r] * Rp[2 * 3 + c];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c)
+                        Mr[r * 3 + c] = rel[r * 3] * A.Kinv[c] + rel[r * 3 + 1] * A.Kinv[3 + c] + rel[r * 3 + 2] * A.Kinv[6 + c];
+                for (int r = 0; r < 3; ++r) vp[r] = Mr[r * 3] * (double)f0 + Mr[r * 3 + 1] * (double)f1 + Mr[r * 3 + 2];
+                double dot = vc[0] * vp[0] + vc[1] * vp[1] + vc[2] * vp[2];
+                double nc = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
+                double np = sqrt(vp[0] * vp[0] + vp[1] * vp[1] + vp[2] * vp[2]);
+                double cs = dot / (nc * np);
+                cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
+                const double ang = acos(cs) * 57.29577951308232;      // np.degrees(np.arccos(.))
+                if (ang < A.min_angle) {
+                    retain = true;
+                } else {
+                    double Rpw[9], tpw[3], Pp[12];
+                    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rpw[r * 3 + c] = Rp[c * 3 + r];
+                    for (int r = 0; r < 3; ++r) tpw[r] = -(Rpw[r * 3] * tp[0] + Rpw[r * 3 + 1] * tp[1] + Rpw[r * 3 + 2] * tp[2]);
+                    for (int r = 0; r < 3; ++r)
+                        for (int c = 0; c < 4; ++c) {
+                            double acc = 0;
+                            for (int q = 0; q < 3; ++q) acc += A.K[r * 3 + q] * (c < 3 ? Rpw[q * 3 + c] : tpw[q]);
+                            Pp[r * 4 + c] = acc;
+                        }
+                    double X4[4];
+                    tri_one(Pp, Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
+                    const float w4 = (float)X4[3];
+                    Xo[0] = (float)X4[0] / w4;
+                    Xo[1] = (float)X4[1] / w4;
+                    Xo[2] = (float)X4[2] / w4;
+                    const double zc = Rcwc[6] * (double)Xo[0] + Rcwc[7] * (double)Xo[1] + Rcwc[8] * (double)Xo[2] + tcwc[2];
+                    const double zp = Rpw[6] * (double)Xo[0] + Rpw[7] * (double)Xo[1] + Rpw[8] * (double)Xo[2] + tpw[2];
+                    if (zc > A.min_d && zp > A.min_d && zc < A.max_d && zp < A.max_d) accept = true;
+                    else retain = true;                               // quirk Q5
+                }
+            }
+        }
+        int tacc, tret;
+        const int pa = nL + block_scan_flag(accept, lds, &tacc);
+        const int pr = kept + block_scan_flag(retain, lds, &tret);
+        if (accept) {
+            if (pa < d.ncap) {
+                X[3 * pa] = Xo[0]; X[3 * pa + 1] = Xo[1]; X[3 * pa + 2] = Xo[2];
+                kp[2 * pa] = k0; kp[2 * pa + 1] = k1;
+            } else {
+                sh_fail = 1;
+            }
+        }
+        if (retain) {
+            ck[2 * pr] = k0; ck[2 * pr + 1] = k1; cf[2 * pr] = f0; cf[2 * pr + 1] = f1; ct[pr] = tau;
+        }
+        nL += tacc;
+        kept += tret;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        s.nL[b] = nL < d.ncap ? nL : d.ncap;
+        s.nC[b] = kept;
+        if (sh_fail) s.status[b] = VO_ST_CAPACITY;
+    }
+}
+
+// ------------------------------------------------ feature adding + step finish
+#define ADD_THREADS 1024
+#define ADD_MAX_CELLS 8192
+#define ADD_MAX_ITEMS 16384
+
+struct AddArgs {
+    vo_dims d;
+    vo_state s;
+    double min_dist;
+    int boot;              // 1: bootstrap finish (no GFTT)
+};
+
+__global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
+{
+    __shared__ int cstart[ADD_MAX_CELLS + 1];
+    __shared__ int cfill[ADD_MAX_CELLS];
+    __shared__ int items[ADD_MAX_ITEMS];
+    __shared__ int lds[16];
+    __shared__ int sh_scan[ADD_THREADS / 64];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    if (s.status[b] != 0) return;
+    const int nF = s.nF[b];
+    const int M = s.nCorners[b];
+    if (M == 0) { if (tid == 0) s.status[b] = VO_ST_GFTT_NONE; return; }   // None.squeeze()
+    if (M == 1) { if (tid == 0) s.status[b] = VO_ST_GFTT_ONE; return; }    // (2,) indexing
+    const int P = s.nC[b];
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    const float* cor = s.corners + (int64_t)b * d.mcap * 2;
+    const float mdf = (float)A.min_dist;
+    const int cs = (int)ceil(A.min_dist) > 0 ? (int)ceil(A.min_dist) : 1;
+    const int gw = d.W / cs + 3, gh = d.H / cs + 3;
+    const bool grid = (gw * gh <= ADD_MAX_CELLS) && (P <= ADD_MAX_ITEMS);
+    if (grid) {
+        for (int q = tid; q < gw * gh; q += blockDim.x) cfill[q] = 0;
+        __syncthreads();
+        for (int i = tid; i < P; i += blockDim.x) {
+            int cx = (int)floorf(ck[2 * i] / (float)cs) + 1, cy = (int)floorf(ck[2 * i + 1] / (float)cs) + 1;
+            cx = cx < 0 ? 0 : (cx > gw - 1 ? gw - 1 : cx);
+            cy = cy < 0 ? 0 : (cy > gh - 1 ? gh - 1 : cy);
+            atomicAdd(&cfill[cy * gw + cx], 1);
+        }
+        __syncthreads();
+        // exclusive scan of cell counts (block-wide, sequential chunks per thread)
+        const int ncell = gw * gh;
+        const int per = (ncell + blockDim.x - 1) / blockDim.x;
+        int local = 0;
+        for (int q = tid * per; q < (tid + 1) * per && q < ncell; ++q) local += cfill[q];
+        int incl = local;
+        for (int o = 1; o < 64; o <<= 1) { int v = __shfl_up(incl, o, 64); if (lane_id() >= o) incl += v; }
+        if (lane_id() == 63) sh_scan[wave_id()] = incl;
+        __syncthreads();
+        int wbase = 0;
+        for (int w = 0; w < wave_id(); ++w) wbase += sh_scan[w];
+        int run = wbase + incl - local;
+        for (int q = tid * per; q < (tid + 1) * per && q < ncell; ++q) { cstart[q] = run; run += cfill[q]; cfill[q] = 0; }
+        if (tid == 0) cstart[ncell] = P;
+        __syncthreads();
+        for (int i = tid; i < P; i += blockDim.x) {
+            int cx = (int)floorf(ck[2 * i] / (float)cs) + 1, cy = (int)floorf(ck[2 * i + 1] / (float)cs) + 1;
+            cx = cx < 0 ? 0 : (cx > gw - 1 ? gw - 1 : cx);
+            cy = cy < 0 ? 0 : (cy > gh - 1 ? gh - 1 : cy);
+            const int cell = cy * gw + cx;
+            items[cstart[cell] + atomicAdd(&cfill[cell], 1)] = i;
+        }
+        __syncthreads();
+    }
+    int nC = P;
+    for (int base = 0; base < M; base += blockDim.x) {
+        const int j = base + tid;
+        bool keep = false;
+        float x = 0, y = 0;
+        if (j < M) {
+            x = cor[2 * j]; y = cor[2 * j + 1];
+            keep = true;
+            if (grid) {
+                const int cx = (int)floorf(x / (float)cs) + 1, cy = (int)floorf(y / (float)cs) + 1;
+                for (int yy = cy - 1; yy <= cy + 1 && keep; ++yy) {
+                    if (yy < 0 || yy >= gh) continue;
+                    for (int xx = cx - 1; xx <= cx + 1 && keep; ++xx) {
+                        if (xx < 0 || xx >= gw) continue;
+                        const int cell = yy * gw + xx;
+                        for (int q = cstart[cell]; q < cstart[cell + 1]; ++q) {
+                            const int i = items[q];
+                            const float dx = x - ck[2 * i], dy = y - ck[2 * i + 1];
+                            if (!(sqrtf(dx * dx + dy * dy) > mdf)) { keep = false; break; }
+                        }
+                    }
+                }
+            } else {
+                for (int i = 0; i < P && keep; ++i) {
+                    const float dx = x - ck[2 * i], dy = y - ck[2 * i + 1];
+                    if (!(sqrtf(dx * dx + dy * dy) > mdf)) keep = false;
+                }
+            }
+        }
+        __syncthreads();   // all reads of ck in this chunk done before appends
+        int tot;
+        const int pos = nC + block_scan_flag(keep, lds, &tot);
+        if (keep && pos < d.pcap) {
+            ck[2 * pos] = x; ck[2 * pos + 1] = y;
+            cf[2 * pos] = x; cf[2 * pos + 1] = y;
+            ct[pos] = nF;                                             // tau = len(transforms)
+        }
+        nC += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (nC > d.pcap) { s.status[b] = VO_ST_CAPACITY; nC = d.pcap; }
+        s.nC[b] = nC;
+        s.num_pts[(int64_t)b * d.fcap + nF] = s.nInl[b];
+        s.nF[b] = nF + 1;
+    }
+}
+
+// cv2.triangulatePoints over independent (P1, P2, x1, x2) rows
+__global__ void k_tri_points(int n, const double* P1, const double* P2, const float* x1, const float* x2, float* out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double X4[4];
+    tri_one(P1 + 12 * i, P2 + 12 * i, x1[2 * i], x1[2 * i + 1], x2[2 * i], x2[2 * i + 1], X4);
+    for (int q = 0; q < 4; ++q) out[4 * i + q] = (float)X4[q];
+}
+
+__global__ void k_rodrigues(int n, int to_matrix, const double* in, double* out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (to_matrix) rodrigues_v2m(in + 3 * i, out + 9 * i);
+    else rodrigues_m2v(in + 9 * i, out + 3 * i);
+}
+
+}  // namespace
+
+// ======================================================================= host side
+#define VO_STREAM(s) ((hipStream_t)(s))
+static inline int hip_rc() { return hipGetLastError() == hipSuccess ? VO_OK : VO_EHIP; }
+
+static void fill_pnp(PnPArgs& P, const vo_opts* o)
+{
+    for (int i = 0; i < 9; ++i) P.K[i] = o->K[i];
+    P.thr = (float)(o->pnp_error * o->pnp_error);
+    P.conf = o->pnp_conf;
+    P.iters = o->pnp_iters;
+}
+
+extern "C" int vo_pnp_ransac(const vo_opts* o, int B, const float* obj, const float* img, const int32_t* counts,
+                             int32_t cap, double* rvec, double* tvec, int32_t* success, uint8_t* inl_mask,
+                             int32_t* n_inl, double* work, int64_t work_stride, vo_stream_t stream)
+{
+    if (!o || B < 1 || !obj || !img || !counts || !rvec || !tvec || !success || !inl_mask || !n_inl || !work) return VO_EARG;
+    if (work_stride < 12LL * cap + 64) return VO_EARG;
+    PnPArgs P;
+    fill_pnp(P, o);
+    P.min_points = 4;
+    P.obj = obj; P.img = img; P.counts = counts; P.cap = cap; P.chain_status = nullptr;
+    P.work = work; P.work_stride = work_stride; P.iwork = nullptr; P.iwork_stride = 0;
+    P.rvec = rvec; P.tvec = tvec; P.success = success; P.mask = inl_mask; P.n_inl = n_inl;
+    hipLaunchKernelGGL(k_pnp_ransac, dim3(B), dim3(256), 0, VO_STREAM(stream), P);
+    return hip_rc();
+}
+
+extern "C" int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    if (d->work_stride < 12LL * d->ncap + 64) return VO_EARG;
+    PnPArgs P;
+    fill_pnp(P, o);
+    P.min_points = 8;                                                   // :342
+    P.obj = s->lm_X; P.img = s->lm_kp; P.counts = s->nL; P.cap = d->ncap; P.chain_status = s->status;
+    P.work = s->work; P.work_stride = d->work_stride; P.iwork = s->iwork; P.iwork_stride = d->iwork_stride;
+    P.rvec = s->pnp_rt; P.tvec = s->pnp_rt + 3LL * d->B;
+    P.success = s->pnp_ok; P.n_inl = s->pnp_ninl; P.mask = s->pnp_mask;
+    hipStream_t st = VO_STREAM(stream);
+    hipLaunchKernelGGL(k_pnp_ransac, dim3(d->B), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(k_pnp_apply, dim3(d->B), dim3(256), 0, st, *d, *s, P.rvec, P.tvec, P.success, P.mask);
+    return hip_rc();
+}
+
+extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    TriArgs A;
+    A.d = *d;
+    A.s = *s;
+    for (int i = 0; i < 9; ++i) { A.K[i] = o->K[i]; A.Kinv[i] = o->K_inv[i]; }
+    A.min_d = o->min_dist_landmarks;
+    A.max_d = o->max_dist_landmarks;
+    A.min_angle = o->min_baseline_angle;
+    A.min_frames = o->min_baseline_frames;
+    A.force = force;
+    hipLaunchKernelGGL(k_triangulate, dim3(d->B), dim3(256), 0, VO_STREAM(stream), A);
+    return hip_rc();
+}
+
+extern "C" int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    AddArgs A;
+    A.d = *d;
+    A.s = *s;
+    A.min_dist = o->feature_min_dist;
+    A.boot = 0;
+    hipLaunchKernelGGL(k_add_finish, dim3(d->B), dim3(ADD_THREADS), 0, VO_STREAM(stream), A);
+    return hip_rc();
+}
+
+extern "C" int vo_triangulate_points(int n, const double* P1, const double* P2, const float* x1, const float* x2,
+                                     float* out4, vo_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!P1 || !P2 || !x1 || !x2 || !out4))) return VO_EARG;
+    if (n == 0) return VO_OK;
+    hipLaunchKernelGGL(k_tri_points, dim3((n + 127) / 128), dim3(128), 0, VO_STREAM(stream), n, P1, P2, x1, x2, out4);
+    return hip_rc();
+}
+
+extern "C" int vo_rodrigues(int n, int to_matrix, const double* in, double* out, vo_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!in || !out))) return VO_EARG;
+    if (n == 0) return VO_OK;
+    hipLaunchKernelGGL(k_rodrigues, dim3((n + 127) / 128), dim3(128), 0, VO_STREAM(stream), n, to_matrix, in, out);
+    return hip_rc();
+}

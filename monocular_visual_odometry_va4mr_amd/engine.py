@@ -1,0 +1,292 @@
+"""Batched, device-resident VO engine: B independent chains stepped together on one GPU.
+
+Host orchestration for the per-frame step of VisualOdometryPipeLine.continuous_operation
+(/root/reference/VisualOdometryPipeLine.py:326-373).  All state lives in HBM as fixed-
+capacity arrays with per-chain device counts (include/vo_hip.h ``vo_state``); a step is a
+fixed sequence of C-ABI launches on one HIP stream with no host synchronisation, so it can
+be captured into a hipGraph (``capture_step``).  PyTorch is used only to allocate device
+memory and to obtain the current stream.
+
+The reference's per-frame control flow maps to stages as
+
+    feature_tracking :271-290   -> vo_pyr_build(cur) + vo_track(prev) + vo_pyr_deriv(cur)
+    PnP step        :338-358    -> vo_pnp
+    triangulation   :366-367    -> vo_triangulate
+    feature_adding  :369        -> vo_gftt(cur) + vo_add_corners_finish (also :371-373)
+
+and runtime ValueErrors of the reference become per-chain status codes (``statuses``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def pyr_max_level(w: int, h: int, win=(15, 15), max_level: int = 3) -> int:
+    """Levels kept by buildOpticalFlowPyramid (stop when the next level is <= winSize)."""
+    sw, sh = w, h
+    for lvl in range(max_level + 1):
+        sw, sh = (sw + 1) // 2, (sh + 1) // 2
+        if sw <= win[0] or sh <= win[1]:
+            return lvl
+    return max_level
+
+
+def make_opts(K: np.ndarray, options: dict) -> L.VoOpts:
+    o = L.VoOpts()
+    K = np.asarray(K, np.float64)
+    Kinv = np.linalg.inv(K)                       # VisualOdometryPipeLine.py:38
+    for i in range(9):
+        o.K[i] = float(K.flat[i])
+        o.K_inv[i] = float(Kinv.flat[i])
+    o.min_dist_landmarks = float(options["min_dist_landmarks"])
+    o.max_dist_landmarks = float(options["max_dist_landmarks"])
+    o.min_baseline_angle = float(options["min_baseline_angle"])
+    o.cos_baseline = math.cos(math.radians(float(options["min_baseline_angle"])))
+    o.min_baseline_frames = int(options["min_baseline_frames"])
+    o.feature_ratio = float(options.get("feature_ratio", 0.8))
+    o.feature_max_corners = int(options["feature_max_corners"])
+    o.feature_quality_level = float(options["feature_quality_level"])
+    o.feature_min_dist = float(options["feature_min_dist"])
+    o.feature_block_size = int(options["feature_block_size"])
+    o.feature_use_harris = int(bool(options["feature_use_harris"]))
+    o.harris_k = 0.04
+    o.win_w, o.win_h = (int(v) for v in options["winSize"])
+    o.max_level = int(options["maxLevel"])
+    ct, cc, ce = options["criteria"]
+    o.crit_type, o.crit_count, o.crit_eps = int(ct), int(cc), float(ce)
+    o.min_eig = 1e-4
+    o.pnp_conf = float(options["PnP_conf"])
+    o.pnp_error = float(options["PnP_error"])
+    o.pnp_iters = int(options["PnP_iterations"])
+    return o
+
+
+class Engine:
+    """B chains of the VO per-frame step on one device."""
+
+    def __init__(self, K, options: dict, width: int, height: int, batch: int = 1, device=None,
+                 ncap: int = 16384, pcap: int = 16384, fcap: int = 8192):
+        if not torch.cuda.is_available():
+            raise RuntimeError("Engine needs a ROCm GPU (no CPU fallback)")
+        self.lib = L.lib()
+        self.device = torch.device(device or "cuda")
+        self.K = np.asarray(K, np.float64)
+        self.options = dict(options)
+        self.B, self.W, self.H = int(batch), int(width), int(height)
+        self.opts = make_opts(self.K, options)
+        d = L.VoDims()
+        d.B, d.W, d.H = self.B, self.W, self.H
+        win = tuple(int(v) for v in options["winSize"])
+        nlev = pyr_max_level(self.W, self.H, win, int(options["maxLevel"])) + 1
+        if nlev > L.VO_MAX_LEVELS:
+            raise ValueError("too many pyramid levels")
+        d.nlev = nlev
+        off = 0
+        w, h = self.W, self.H
+        for lv in range(nlev):
+            pitch = ((w + 2 * L.VO_BORDER + 63) // 64) * 64
+            d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv] = w, h, pitch, off
+            off += (h + 2 * L.VO_BORDER) * pitch
+            w, h = (w + 1) // 2, (h + 1) // 2
+        d.pyr_stride = ((off + 255) // 256) * 256
+        d.der_stride = 2 * d.pyr_stride
+        d.ncap, d.pcap, d.fcap = int(ncap), int(pcap), int(fcap)
+        d.ccap = self.W * self.H // 2 + 1024
+        mc = int(options["feature_max_corners"])
+        d.mcap = max(1, min(mc if mc > 0 else 8192, 8192))
+        kmax = max(ncap, pcap)
+        d.work_stride = 16 * kmax + 4096
+        d.iwork_stride = 2 * kmax + 4096
+        self.dims = d
+        B = self.B
+        dev = self.device
+        z = lambda *shape, dt: torch.zeros(*shape, dtype=dt, device=dev)
+        T = {}
+        T["pyr0"] = z(B, d.pyr_stride, dt=torch.uint8)
+        T["pyr1"] = z(B, d.pyr_stride, dt=torch.uint8)
+        T["der"] = z(B, d.der_stride, dt=torch.int16)
+        T["lm_X"] = z(B, ncap, 3, dt=torch.float32)
+        T["lm_kp"] = z(B, ncap, 2, dt=torch.float32)
+        T["nL"] = z(B, dt=torch.int32)
+        T["c_kp"] = z(B, pcap, 2, dt=torch.float32)
+        T["c_first"] = z(B, pcap, 2, dt=torch.float32)
+        T["c_tau"] = z(B, pcap, dt=torch.int32)
+        T["nC"] = z(B, dt=torch.int32)
+        T["pose_R"] = z(B, fcap, 9, dt=torch.float64)
+        T["pose_t"] = z(B, fcap, 3, dt=torch.float64)
+        T["nF"] = z(B, dt=torch.int32)
+        T["num_pts"] = z(B, fcap, dt=torch.int32)
+        T["outl_kp"] = z(B, kmax, 2, dt=torch.float32)
+        T["inl_kp"] = z(B, kmax, 2, dt=torch.float32)
+        T["nOutl"] = z(B, dt=torch.int32)
+        T["nInl"] = z(B, dt=torch.int32)
+        T["status"] = z(B, dt=torch.int32)
+        T["trk_pts"] = z(B, ncap + pcap, 2, dt=torch.float32)
+        T["trk_st"] = z(B, ncap + pcap, dt=torch.uint8)
+        T["trk_err"] = z(B, ncap + pcap, dt=torch.float32)
+        T["eig"] = z(B, self.W * self.H, dt=torch.float32)
+        T["eig_max"] = z(B, dt=torch.int32)
+        T["gf_keys"] = z(B, d.ccap, dt=torch.int64)
+        T["gf_n"] = z(B, dt=torch.int32)
+        T["corners"] = z(B, d.mcap, 2, dt=torch.float32)
+        T["nCorners"] = z(B, dt=torch.int32)
+        T["pnp_rt"] = z(2, B, 3, dt=torch.float64)
+        T["pnp_ok"] = z(B, dt=torch.int32)
+        T["pnp_ninl"] = z(B, dt=torch.int32)
+        T["pnp_mask"] = z(B, ncap, dt=torch.uint8)
+        T["work"] = z(B, d.work_stride, dt=torch.float64)
+        T["iwork"] = z(B, d.iwork_stride, dt=torch.int32)
+        self.t = T
+        s = L.VoState()
+        for name in L._STATE_FIELDS:
+            setattr(s, name, T[name].data_ptr())
+        self.state = s
+        self.prev = 0                      # index of the pyramid holding potential_frame
+        self._pd, self._po, self._ps = C.byref(self.dims), C.byref(self.opts), C.byref(self.state)
+        self._graphs = {}
+
+    # ------------------------------------------------------------------ utils
+    @property
+    def stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _chk(self, rc, what):
+        L.check(rc, what)
+
+    def statuses(self) -> np.ndarray:
+        return self.t["status"].cpu().numpy()
+
+    # ------------------------------------------------------------------ stages
+    def build_pyramid(self, frames: torch.Tensor, which: int, deriv: bool = False):
+        frames = self._frames(frames)
+        self._chk(self.lib.vo_pyr_build(self._pd, self._ps, which, C.c_void_p(frames.data_ptr()),
+                                        self.W * self.H, self.stream), "vo_pyr_build")
+        if deriv:
+            self._chk(self.lib.vo_pyr_deriv(self._pd, self._ps, which, self.stream), "vo_pyr_deriv")
+
+    def _frames(self, frames):
+        if not isinstance(frames, torch.Tensor):
+            frames = torch.as_tensor(np.ascontiguousarray(frames))
+        if frames.dim() == 2:
+            frames = frames.unsqueeze(0)
+        if frames.dtype != torch.uint8 or tuple(frames.shape) != (self.B, self.H, self.W):
+            raise ValueError(f"frames must be uint8 [{self.B},{self.H},{self.W}]")
+        return frames.to(self.device, non_blocking=True).contiguous()
+
+    def step(self, frames):
+        """One continuous_operation for every chain (frames: uint8 [B,H,W], any device)."""
+        frames = self._frames(frames)
+        self._step_launch(frames, self.prev)
+        self.prev = 1 - self.prev
+
+    def _step_launch(self, frames, prev):
+        cur = 1 - prev
+        lib, st = self.lib, self.stream
+        pd, po, ps = self._pd, self._po, self._ps
+        self._chk(lib.vo_pyr_build(pd, ps, cur, C.c_void_p(frames.data_ptr()), self.W * self.H, st), "vo_pyr_build")
+        self._chk(lib.vo_track(pd, po, ps, prev, st), "vo_track")
+        self._chk(lib.vo_pyr_deriv(pd, ps, cur, st), "vo_pyr_deriv")
+        self._chk(lib.vo_pnp(pd, po, ps, st), "vo_pnp")
+        self._chk(lib.vo_triangulate(pd, po, ps, 0, st), "vo_triangulate")
+        self._chk(lib.vo_gftt(pd, po, ps, cur, st), "vo_gftt")
+        self._chk(lib.vo_add_corners_finish(pd, po, ps, st), "vo_add_corners_finish")
+
+    def capture_step(self):
+        """Capture the two ping-pong variants of the step into hipGraphs; returns a
+        replay function taking a device frame buffer already bound at capture time."""
+        buf = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=self.device)
+        graphs = []
+        side = torch.cuda.Stream(self.device)
+        for prev in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side):
+                    self._step_launch(buf, prev)
+            graphs.append(g)
+        torch.cuda.synchronize(self.device)
+        self._graphs = {"buf": buf, "g": graphs}
+        return buf
+
+    def replay_step(self):
+        g = self._graphs["g"][self.prev]
+        g.replay()
+        self.prev = 1 - self.prev
+
+    # ------------------------------------------------------------------ state I/O
+    def import_chain(self, b: int, *, landmarks, keypoints, cand, cand_first, cand_tau, transforms,
+                     num_pts, prev_img):
+        """Load reference-shaped state into chain b (checkpoint restore / test hook)."""
+        d = self.dims
+        T = self.t
+        lm = np.asarray(landmarks, np.float32).reshape(-1, 3)
+        kp = np.asarray(keypoints, np.float32).reshape(-1, 2)
+        c = np.asarray(cand, np.float32).reshape(-1, 2)
+        cf = np.asarray(cand_first, np.float32).reshape(-1, 2)
+        ct = np.asarray(cand_tau).reshape(-1).astype(np.int32)
+        if lm.shape[0] > d.ncap or c.shape[0] > d.pcap or len(transforms) >= d.fcap:
+            raise ValueError("state exceeds engine capacity")
+        dev = self.device
+        T["lm_X"][b, :lm.shape[0]] = torch.from_numpy(lm).to(dev)
+        T["lm_kp"][b, :kp.shape[0]] = torch.from_numpy(kp).to(dev)
+        T["nL"][b] = lm.shape[0]
+        T["c_kp"][b, :c.shape[0]] = torch.from_numpy(c).to(dev)
+        T["c_first"][b, :cf.shape[0]] = torch.from_numpy(cf).to(dev)
+        T["c_tau"][b, :ct.shape[0]] = torch.from_numpy(ct).to(dev)
+        T["nC"][b] = c.shape[0]
+        Rs = np.stack([np.asarray(R, np.float64).reshape(9) for R, _ in transforms])
+        ts = np.stack([np.asarray(t, np.float64).reshape(3) for _, t in transforms])
+        T["pose_R"][b, :len(transforms)] = torch.from_numpy(Rs).to(dev)
+        T["pose_t"][b, :len(transforms)] = torch.from_numpy(ts).to(dev)
+        T["nF"][b] = len(transforms)
+        npts = np.asarray(num_pts, np.int32).reshape(-1)
+        if npts.size:
+            T["num_pts"][b, 1:1 + npts.size] = torch.from_numpy(npts).to(dev)
+        T["status"][b] = 0
+        img = torch.as_tensor(np.ascontiguousarray(prev_img, np.uint8)).to(dev)
+        # rebuild the potential_frame pyramid + derivatives for this chain only
+        full = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=dev)
+        full[b] = img
+        keep = T["pyr%d" % self.prev].clone(), T["der"].clone()
+        self.build_pyramid(full, self.prev, deriv=True)
+        mask = torch.zeros(self.B, dtype=torch.bool, device=dev)
+        mask[b] = True
+        T["pyr%d" % self.prev][~mask] = keep[0][~mask]
+        T["der"][~mask] = keep[1][~mask]
+
+    def export_chain(self, b: int) -> dict:
+        T = self.t
+        torch.cuda.synchronize(self.device)
+        nL, nC, nF = int(T["nL"][b]), int(T["nC"][b]), int(T["nF"][b])
+        nI, nO = int(T["nInl"][b]), int(T["nOutl"][b])
+        R = T["pose_R"][b, :nF].cpu().numpy().reshape(-1, 3, 3)
+        t = T["pose_t"][b, :nF].cpu().numpy().reshape(-1, 3, 1)
+        return {
+            "landmarks": T["lm_X"][b, :nL].cpu().numpy(),
+            "keypoints": T["lm_kp"][b, :nL].cpu().numpy(),
+            "cand": T["c_kp"][b, :nC].cpu().numpy(),
+            "cand_first": T["c_first"][b, :nC].cpu().numpy(),
+            "cand_tau": T["c_tau"][b, :nC].cpu().numpy().astype(np.float64).reshape(-1, 1),
+            "transforms": [(R[i], t[i]) for i in range(nF)],
+            "num_pts": T["num_pts"][b, 1:nF].cpu().numpy(),
+            "inliers": T["inl_kp"][b, :nI].cpu().numpy(),
+            "outliers": T["outl_kp"][b, :nO].cpu().numpy(),
+            "status": int(T["status"][b]),
+        }
+
+    def pyramid_level(self, which: int, level: int, b: int = 0) -> np.ndarray:
+        d = self.dims
+        w, h, p, o = d.lvl_w[level], d.lvl_h[level], d.lvl_pitch[level], d.lvl_off[level]
+        buf = self.t["pyr%d" % which][b, o:o + (h + 2 * L.VO_BORDER) * p].view(h + 2 * L.VO_BORDER, p)
+        return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()
+
+    def deriv_level(self, level: int, b: int = 0) -> np.ndarray:
+        d = self.dims
+        w, h, p, o = d.lvl_w[level], d.lvl_h[level], d.lvl_pitch[level], d.lvl_off[level]
+        buf = self.t["der"][b, 2 * o:2 * (o + (h + 2 * L.VO_BORDER) * p)].view(h + 2 * L.VO_BORDER, p, 2)
+        return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()

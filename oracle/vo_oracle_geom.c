@@ -19,8 +19,9 @@
  *     via rvec -> Rodrigues -> R, a ~1e-16 relative round trip).
  *   - Real quartic roots (P3P) come from a bracketed Newton/bisection solver that
  *     uses only + - * / sqrt (OpenCV: closed-form Ferrari).
- *   - Sums over points inside EPnP use a fixed "256 strided partials + pairwise
- *     tree" order so CPU and GPU agree bit for bit.
+ *   - Sums over points inside EPnP use a fixed order -- item i goes to partial
+ *     (i % 64), then a pairwise tree 32,16,..,1 -- which is exactly one 64-lane
+ *     wave's strided accumulation + shuffle tree on the GPU.
  */
 #include "vo_oracle.h"
 
@@ -29,7 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define NPART 256
+#define NPART 64
 
 /* ================================================================ linalg */
 
@@ -522,8 +523,8 @@ int vo_o_p3p(const double* K, const double* obj4, const double* img4, double* R,
 
 /* ================================================================ EPnP */
 
-/* deterministic sum over n items of K-vectors: item i -> partial (i % 256), then a
- * pairwise tree 128,64,...,1.  contrib(i, out[K]) supplies item i's vector. */
+/* deterministic sum over n items of K-vectors: item i -> partial (i % 64), then a
+ * pairwise tree 32,16,...,1.  contrib(i, out[K]) supplies item i's vector. */
 typedef void (*contrib_fn)(const void* ctx, int i, double* out);
 
 static void det_sum(const void* ctx, contrib_fn f, int n, int K, double* out)
