@@ -176,35 +176,47 @@ int vo_rodrigues(int n, int to_matrix, const double* in, double* out, vo_stream_
 
 /* ---- bootstrap (initialization, :293-323) --------------------------------------- */
 
+/* Device buffers for one SIFT invocation.  Geometry (octave sizes/offsets) is filled by
+ * vo_sift_plan(); the buffers are caller-allocated with the sizes it reports. */
+#define VO_SIFT_MAX_OCT 16
 typedef struct vo_sift_buf {
-    float* gauss;                 /* octave-layer Gaussian images, packed              */
-    float* dog;                   /* DoG images, packed                                */
-    float* tmp;                   /* blur scratch                                      */
-    int64_t gauss_off[16 * 6], dog_off[16 * 5];
-    int32_t oct_w[16], oct_h[16];
+    int32_t W, H;                 /* input image size                                   */
     int32_t n_oct;
-    float* kern;                  /* Gaussian kernels [6][64] (host-computed, exp())   */
-    int32_t ksize[6];
-    float* exptab;                /* exp32f table [64]                                 */
-    int32_t* cand;                /* extrema candidates [cand_cap][4]                  */
-    int32_t* n_cand;
-    float* kp;                    /* raw keypoints [kp_cap][8]                         */
-    int32_t* n_kp;
-    int32_t* order;               /* sort permutation [kp_cap]                         */
-    float* kp_out;                /* sorted, deduplicated keypoints [kp_cap][6]        */
-    float* desc;                  /* descriptors [kp_cap][128]                         */
-    int32_t* n_out;
-    float* hist_scratch;          /* [kp_cap][360]                                     */
+    int32_t oct_w[VO_SIFT_MAX_OCT], oct_h[VO_SIFT_MAX_OCT];
+    int64_t gauss_off[VO_SIFT_MAX_OCT * 6];   /* float offsets into gauss            */
+    int64_t dog_off[VO_SIFT_MAX_OCT * 5];     /* float offsets into dog              */
+    int64_t gauss_floats, dog_floats, tmp_floats;
+    float* gauss;                 /* Gaussian scale space                               */
+    float* dog;                   /* difference of Gaussians                            */
+    float* tmp;                   /* separable-blur scratch (2W*2H floats)              */
+    float* consts;                /* [7*32 kernel taps][64 exp32f table] (host-filled)  */
+    int32_t* counters;            /* [4]: n_cand, n_kp, n_out, overflow                 */
+    int32_t* cand;                /* extrema candidates [cand_cap][4] (o, layer, r, c)  */
+    float* kp;                    /* raw keypoints [kp_cap][8]                          */
+    float* kp_out;                /* sorted, deduplicated keypoints [kp_cap][6]         */
+    float* desc;                  /* descriptors [kp_cap][128] (integer-valued floats)  */
+    float* hist;                  /* descriptor histogram scratch [kp_cap][360]         */
     int32_t cand_cap, kp_cap;
 } vo_sift_buf;
+
+/* Fill the geometry of `sb` for a W x H image (host only, no device work). */
+int vo_sift_plan(vo_sift_buf* sb, int W, int H);
 
 /* cv2.SIFT_create().detectAndCompute(img, None) (:35,226-227) for one image. */
 int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream);
 
-/* BFMatcher().knnMatch(q, t, k=2) (:36,229): integer-valued float descriptors,
- * MFMA distance matrix; out idx [nq][2], dist [nq][2]. counts read on device. */
+/* BFMatcher().knnMatch(q, t, k=2) (:36,229) for integer-valued float descriptors of
+ * dim 128: bf16 MFMA distance tiles (exact), top-2 per query with OpenCV's tie order.
+ * nq/nt are read on the device; idx2 [qcap][2] (-1 if absent), dist2 [qcap][2]. */
 int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt,
                int32_t qcap, int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream);
+
+/* Ratio test + match gathering of initial_feature_matching (:218-245) for B chains:
+ * keeps query i iff dist0 < ratio * dist1 (in double, as Python), in query order. */
+int vo_ratio_matches(int B, const float* kp0, const float* kp1, int32_t kp_stride,
+                     const int32_t* idx2, const float* dist2, const int32_t* nq, int32_t q_stride,
+                     double ratio, float* pts0, float* pts1, int32_t* counts, int32_t cap,
+                     vo_stream_t stream);
 
 /* cv2.findEssentialMat(p0,p1,K,RANSAC,prob,threshold) (:308) for B problems of
  * [B][cap] points with counts; E [B][9], mask [B][cap]. */

@@ -81,6 +81,21 @@ class VoState(C.Structure):
     _fields_ = [(n, vp) for n in _STATE_FIELDS]
 
 
+VO_SIFT_MAX_OCT = 16
+
+
+class VoSiftBuf(C.Structure):
+    _fields_ = [
+        ("W", i32), ("H", i32), ("n_oct", i32),
+        ("oct_w", i32 * VO_SIFT_MAX_OCT), ("oct_h", i32 * VO_SIFT_MAX_OCT),
+        ("gauss_off", i64 * (VO_SIFT_MAX_OCT * 6)), ("dog_off", i64 * (VO_SIFT_MAX_OCT * 5)),
+        ("gauss_floats", i64), ("dog_floats", i64), ("tmp_floats", i64),
+        ("gauss", vp), ("dog", vp), ("tmp", vp), ("consts", vp), ("counters", vp), ("cand", vp),
+        ("kp", vp), ("kp_out", vp), ("desc", vp), ("hist", vp),
+        ("cand_cap", i32), ("kp_cap", i32),
+    ]
+
+
 _lib = None
 
 
@@ -124,9 +139,12 @@ def _declare(L):
         "vo_triangulate_points": ([C.c_int, P, P, P, P, P, P], C.c_int),
         "vo_rodrigues": ([C.c_int, C.c_int, P, P, P], C.c_int),
     }
+    SB = C.POINTER(VoSiftBuf)
     optional = {
-        "vo_sift": ([P, P, C.c_int, C.c_int, P], C.c_int),
+        "vo_sift_plan": ([SB, C.c_int, C.c_int], C.c_int),
+        "vo_sift": ([SB, P, C.c_int, C.c_int, P], C.c_int),
         "vo_bf_knn2": ([P, P, P, P, i32, i32, P, P, P], C.c_int),
+        "vo_ratio_matches": ([C.c_int, P, P, i32, P, P, P, i32, f64, P, P, P, i32, P], C.c_int),
         "vo_find_essential": ([O, C.c_int, P, P, P, i32, f64, f64, i32, P, P, P, P, i32, P], C.c_int),
         "vo_recover_pose": ([O, C.c_int, P, P, P, P, i32, P, P, P, P, P], C.c_int),
         "vo_bootstrap": ([D, O, S, P, P, P, i32, P], C.c_int),

@@ -1,0 +1,763 @@
+// SIFT (OpenCV 4.6 defaults) and brute-force 2-NN matching for gfx950
+// (VisualOdometryPipeLine.py:35-36, :209-245).  SIFT stages: exact 2x upsample,
+// separable Gaussian scale space (taps summed in a fixed order), DoG, 26-neighbour
+// extrema (atomic candidate append -- order is irrelevant because keypoints are
+// canonically sorted), per-candidate refinement + orientation histogram, LDS bitonic
+// sort + dedupe (KeyPointsFilter::removeDuplicatedSorted), per-keypoint descriptor.
+// Every float operation mirrors oracle/vo_oracle_sift.c.
+//
+// The matcher computes the query x train dot products with v_mfma_f32_32x32x16_bf16:
+// SIFT descriptor entries are integers 0..255 (exact in bf16) and sums stay below 2^24,
+// so distances are exact; the per-query top-2 scan keeps OpenCV's tie order.
+#include "vo_dev.h"
+
+#include <float.h>
+#include <limits.h>
+#include <math.h>
+#include <string.h>
+
+#define N_LAYERS 3
+#define SIFT_IMG_BORDER 5
+#define SIFT_MAX_INTERP_STEPS 5
+#define SIFT_ORI_HIST_BINS 36
+#define SIFT_ORI_SIG_FCTR 1.5f
+#define SIFT_ORI_RADIUS (3 * SIFT_ORI_SIG_FCTR)
+#define SIFT_ORI_PEAK_RATIO 0.8f
+#define SIFT_DESCR_SCL_FCTR 3.f
+#define SIFT_DESCR_MAG_THR 0.2f
+#define SIFT_INT_DESCR_FCTR 512.f
+#define KTAPS 32
+#define EXPTAB_OFF (7 * KTAPS)
+
+namespace {
+
+// ------------------------------------------------------- exp32f / fastAtan2 (OpenCV)
+#define EXPPOLY_32F_A0 .9670371139572337719125840413672004409288e-2
+
+VO_DEV float exp32f(float x, const float* tab)
+{
+    const float A4 = (float)(1.000000000000002438532970795181890933776 / EXPPOLY_32F_A0);
+    const float A3 = (float)(.6931471805521448196800669615864773144641 / EXPPOLY_32F_A0);
+    const float A2 = (float)(.2402265109513301490103372422686535526573 / EXPPOLY_32F_A0);
+    const float A1 = (float)(.5550339366753125211915322047004666939128e-1 / EXPPOLY_32F_A0);
+    const float prescale = (float)(1.4426950408889634073599246810019 * (1 << 6));
+    const float postscale = (float)(1. / (1 << 6));
+    float x0 = x * prescale;
+    int xi = __float2int_rn(x0);
+    x0 = (x0 - (float)xi) * postscale;
+    int t = (xi >> 6) + 127;
+    t = !(t & ~255) ? t : (t < 0 ? 0 : 255);
+    const float two = __int_as_float(t << 23);
+    return two * tab[xi & 63] * ((((x0 + A1) * x0 + A2) * x0 + A3) * x0 + A4);
+}
+
+VO_DEV float fast_atan2(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ------------------------------------------------------- scale space
+__global__ void k_upsample(const uint8_t* __restrict__ img, int w, int h, float* __restrict__ dst)
+{
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x, dy = blockIdx.y;
+    const int dw = 2 * w;
+    if (dx >= dw) return;
+    float fy = (float)((dy + 0.5) * 0.5 - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= sy;
+    if (sy < 0) { fy = 0; sy = 0; }
+    if (sy >= h - 1) { fy = 0; sy = h - 1; }
+    const int sy1 = sy + 1 < h ? sy + 1 : h - 1;
+    float fx = (float)((dx + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx >= w - 1) { fx = 0; sx = w - 1; }
+    const int sx1 = sx + 1 < w ? sx + 1 : w - 1;
+    const uint8_t* r0 = img + (int64_t)sy * w;
+    const uint8_t* r1 = img + (int64_t)sy1 * w;
+    const float v0 = (float)r0[sx] * (1.f - fx) + (float)r0[sx1] * fx;
+    const float v1 = (float)r1[sx] * (1.f - fx) + (float)r1[sx1] * fx;
+    dst[(int64_t)dy * dw + dx] = v0 * (1.f - fy) + v1 * fy;
+}
+
+__global__ void k_blur_h(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
+                         const float* __restrict__ kern, int n)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const int r = n / 2;
+    const float* s = src + (int64_t)y * w;
+    float acc = 0.f;
+    for (int i = 0; i < n; ++i) acc += kern[i] * s[refl101(x - r + i, w)];
+    dst[(int64_t)y * w + x] = acc;
+}
+
+__global__ void k_blur_v(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
+                         const float* __restrict__ kern, int n)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const int r = n / 2;
+    float acc = 0.f;
+    for (int i = 0; i < n; ++i) acc += kern[i] * src[(int64_t)refl101(y - r + i, h) * w + x];
+    dst[(int64_t)y * w + x] = acc;
+}
+
+__global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh)
+{
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+    if (x >= dw) return;
+    const double ifx = 1. / ((double)dw / sw), ify = 1. / ((double)dh / sh);
+    int sy = (int)floor(y * ify);
+    if (sy > sh - 1) sy = sh - 1;
+    int sx = (int)floor(x * ifx);
+    if (sx > sw - 1) sx = sw - 1;
+    dst[(int64_t)y * dw + x] = src[(int64_t)sy * sw + sx];
+}
+
+__global__ void k_dog(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ d, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) d[i] = b[i] - a[i];
+}
+
+__global__ void k_extrema(vo_sift_buf sb, int o, int layer)
+{
+    const int w = sb.oct_w[o], h = sb.oct_h[o];
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + SIFT_IMG_BORDER;
+    const int r = blockIdx.y + SIFT_IMG_BORDER;
+    if (c >= w - SIFT_IMG_BORDER || r >= h - SIFT_IMG_BORDER) return;
+    const int idx = o * (N_LAYERS + 2) + layer;
+    const float* img = sb.dog + sb.dog_off[idx];
+    const float* prev = sb.dog + sb.dog_off[idx - 1];
+    const float* next = sb.dog + sb.dog_off[idx + 1];
+    const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
+    const float val = img[(int64_t)r * w + c];
+    if (!(fabsf(val) > threshold)) return;
+    bool ext = true;
+    for (int dz = 0; dz < 3 && ext; ++dz) {
+        const float* L = dz == 0 ? prev : (dz == 1 ? img : next);
+        for (int dy = -1; dy <= 1 && ext; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                const float u = L[(int64_t)(r + dy) * w + (c + dx)];
+                if (val > 0 ? !(val >= u) : !(val <= u)) { ext = false; break; }
+            }
+    }
+    if (!ext) return;
+    const int k = atomicAdd(&sb.counters[0], 1);
+    if (k < sb.cand_cap) {
+        sb.cand[4 * k] = o; sb.cand[4 * k + 1] = layer; sb.cand[4 * k + 2] = r; sb.cand[4 * k + 3] = c;
+    } else {
+        sb.counters[3] = 1;
+    }
+}
+
+// ------------------------------------------------------- keypoints
+#define DAT(base, w, r, c) ((base)[(int64_t)(r) * (w) + (c)])
+
+VO_DEV void lu3_solve(float A[9], float b[3], float X[3])
+{
+    const float eps = FLT_EPSILON * 10;
+    for (int i = 0; i < 3; ++i) {
+        int k = i;
+        for (int j = i + 1; j < 3; ++j) if (fabsf(A[j * 3 + i]) > fabsf(A[k * 3 + i])) k = j;
+        if (fabsf(A[k * 3 + i]) < eps) { X[0] = X[1] = X[2] = 0; return; }
+        if (k != i) {
+            for (int j = i; j < 3; ++j) { float t = A[i * 3 + j]; A[i * 3 + j] = A[k * 3 + j]; A[k * 3 + j] = t; }
+            float t = b[i]; b[i] = b[k]; b[k] = t;
+        }
+        float d = -1 / A[i * 3 + i];
+        for (int j = i + 1; j < 3; ++j) {
+            float alpha = A[j * 3 + i] * d;
+            for (int kk = i + 1; kk < 3; ++kk) A[j * 3 + kk] += alpha * A[i * 3 + kk];
+            b[j] += alpha * b[i];
+        }
+        A[i * 3 + i] = -d;
+    }
+    for (int i = 2; i >= 0; --i) {
+        float s = b[i];
+        for (int kk = i + 1; kk < 3; ++kk) s -= A[i * 3 + kk] * b[kk];
+        b[i] = s * A[i * 3 + i];
+    }
+    X[0] = b[0]; X[1] = b[1]; X[2] = b[2];
+}
+
+struct KP { float x, y, size, angle, response; int octave; };
+
+VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, KP& kpt, int octv, int& layer, int& r, int& c, float sigma)
+{
+    const float contrastThreshold = 0.04f, edgeThreshold = 10.f;
+    const float img_scale = 1.f / (255 * 1);
+    const float deriv_scale = img_scale * 0.5f;
+    const float second_deriv_scale = img_scale;
+    const float cross_deriv_scale = img_scale * 0.25f;
+    const int w = sb.oct_w[octv], h = sb.oct_h[octv];
+    float xi = 0, xr = 0, xc = 0, contr = 0;
+    int i = 0;
+    for (; i < SIFT_MAX_INTERP_STEPS; ++i) {
+        const int idx = octv * (N_LAYERS + 2) + layer;
+        const float* img = sb.dog + sb.dog_off[idx];
+        const float* prev = sb.dog + sb.dog_off[idx - 1];
+        const float* next = sb.dog + sb.dog_off[idx + 1];
+        float dD[3] = {(DAT(img, w, r, c + 1) - DAT(img, w, r, c - 1)) * deriv_scale,
+                       (DAT(img, w, r + 1, c) - DAT(img, w, r - 1, c)) * deriv_scale,
+                       (DAT(next, w, r, c) - DAT(prev, w, r, c)) * deriv_scale};
+        float v2 = DAT(img, w, r, c) * 2;
+        float dxx = (DAT(img, w, r, c + 1) + DAT(img, w, r, c - 1) - v2) * second_deriv_scale;
+        float dyy = (DAT(img, w, r + 1, c) + DAT(img, w, r - 1, c) - v2) * second_deriv_scale;
+        float dss = (DAT(next, w, r, c) + DAT(prev, w, r, c) - v2) * second_deriv_scale;
+        float dxy = (DAT(img, w, r + 1, c + 1) - DAT(img, w, r + 1, c - 1) - DAT(img, w, r - 1, c + 1) +
+                     DAT(img, w, r - 1, c - 1)) * cross_deriv_scale;
+        float dxs = (DAT(next, w, r, c + 1) - DAT(next, w, r, c - 1) - DAT(prev, w, r, c + 1) +
+                     DAT(prev, w, r, c - 1)) * cross_deriv_scale;
+        float dys = (DAT(next, w, r + 1, c) - DAT(next, w, r - 1, c) - DAT(prev, w, r + 1, c) +
+                     DAT(prev, w, r - 1, c)) * cross_deriv_scale;
+        float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+        float X[3];
+        lu3_solve(H, dD, X);
+        xi = -X[2]; xr = -X[1]; xc = -X[0];
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3))
+            return false;
+        c += __float2int_rn(xc);
+        r += __float2int_rn(xr);
+        layer += __float2int_rn(xi);
+        if (layer < 1 || layer > N_LAYERS || c < SIFT_IMG_BORDER || c >= w - SIFT_IMG_BORDER || r < SIFT_IMG_BORDER ||
+            r >= h - SIFT_IMG_BORDER)
+            return false;
+    }
+    if (i >= SIFT_MAX_INTERP_STEPS) return false;
+    {
+        const int idx = octv * (N_LAYERS + 2) + layer;
+        const float* img = sb.dog + sb.dog_off[idx];
+        const float* prev = sb.dog + sb.dog_off[idx - 1];
+        const float* next = sb.dog + sb.dog_off[idx + 1];
+        float dD[3] = {(DAT(img, w, r, c + 1) - DAT(img, w, r, c - 1)) * deriv_scale,
+                       (DAT(img, w, r + 1, c) - DAT(img, w, r - 1, c)) * deriv_scale,
+                       (DAT(next, w, r, c) - DAT(prev, w, r, c)) * deriv_scale};
+        float t = dD[0] * xc + dD[1] * xr + dD[2] * xi;
+        contr = DAT(img, w, r, c) * img_scale + t * 0.5f;
+        if (fabsf(contr) * N_LAYERS < contrastThreshold) return false;
+        float v2 = DAT(img, w, r, c) * 2.f;
+        float dxx = (DAT(img, w, r, c + 1) + DAT(img, w, r, c - 1) - v2) * second_deriv_scale;
+        float dyy = (DAT(img, w, r + 1, c) + DAT(img, w, r - 1, c) - v2) * second_deriv_scale;
+        float dxy = (DAT(img, w, r + 1, c + 1) - DAT(img, w, r + 1, c - 1) - DAT(img, w, r - 1, c + 1) +
+                     DAT(img, w, r - 1, c - 1)) * cross_deriv_scale;
+        float tr = dxx + dyy;
+        float det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * edgeThreshold >= (edgeThreshold + 1) * (edgeThreshold + 1) * det) return false;
+    }
+    kpt.x = ((float)c + xc) * (float)(1 << octv);
+    kpt.y = ((float)r + xr) * (float)(1 << octv);
+    kpt.octave = octv + (layer << 8) + ((int)rint((xi + 0.5) * 255) << 16);
+    kpt.size = sigma * (float)pow(2.0, (double)(((float)layer + xi) / N_LAYERS)) * (float)(1 << octv) * 2;
+    kpt.response = fabsf(contr);
+    return true;
+}
+
+VO_DEV float orientation_hist(const float* img, int w, int h, int px, int py, int radius, float sigma, float* hist,
+                              const float* tab)
+{
+    const int n = SIFT_ORI_HIST_BINS;
+    float expf_scale = -1.f / (2.f * sigma * sigma);
+    float th[SIFT_ORI_HIST_BINS + 4];
+    float* temphist = th + 2;
+    for (int i = 0; i < n; ++i) temphist[i] = 0.f;
+    for (int i = -radius; i <= radius; ++i) {
+        int y = py + i;
+        if (y <= 0 || y >= h - 1) continue;
+        for (int j = -radius; j <= radius; ++j) {
+            int x = px + j;
+            if (x <= 0 || x >= w - 1) continue;
+            float dx = DAT(img, w, y, x + 1) - DAT(img, w, y, x - 1);
+            float dy = DAT(img, w, y - 1, x) - DAT(img, w, y + 1, x);
+            float wt = exp32f((float)(i * i + j * j) * expf_scale, tab);
+            float ori = fast_atan2(dy, dx);
+            float mag = sqrtf(dx * dx + dy * dy);
+            int bin = __float2int_rn((n / 360.f) * ori);
+            if (bin >= n) bin -= n;
+            if (bin < 0) bin += n;
+            temphist[bin] += wt * mag;
+        }
+    }
+    temphist[-1] = temphist[n - 1];
+    temphist[-2] = temphist[n - 2];
+    temphist[n] = temphist[0];
+    temphist[n + 1] = temphist[1];
+    for (int i = 0; i < n; ++i)
+        hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) + (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) +
+                  temphist[i] * (6.f / 16.f);
+    float maxval = hist[0];
+    for (int i = 1; i < n; ++i) maxval = maxval > hist[i] ? maxval : hist[i];
+    return maxval;
+}
+
+__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nc = min(sb.counters[0], sb.cand_cap);
+    if (k >= nc) return;
+    const float* tab = sb.consts + EXPTAB_OFF;
+    const int o = sb.cand[4 * k], i0 = sb.cand[4 * k + 1];
+    int r1 = sb.cand[4 * k + 2], c1 = sb.cand[4 * k + 3], layer = i0;
+    KP kpt;
+    if (!adjust_local_extrema(sb, kpt, o, layer, r1, c1, 1.6f)) return;
+    const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
+    float hist[SIFT_ORI_HIST_BINS];
+    const float* g = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
+    const float omax = orientation_hist(g, sb.oct_w[o], sb.oct_h[o], c1, r1, __float2int_rn(SIFT_ORI_RADIUS * scl_octv),
+                                        SIFT_ORI_SIG_FCTR * scl_octv, hist, tab);
+    const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
+    const int n = SIFT_ORI_HIST_BINS;
+    for (int j = 0; j < n; ++j) {
+        const int l = j > 0 ? j - 1 : n - 1;
+        const int r2 = j < n - 1 ? j + 1 : 0;
+        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+            float angle = 360.f - (float)((360.f / n) * bin);
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            const int q = atomicAdd(&sb.counters[1], 1);
+            if (q < sb.kp_cap) {
+                float* out = sb.kp + 8 * (int64_t)q;
+                out[0] = kpt.x; out[1] = kpt.y; out[2] = kpt.size; out[3] = angle; out[4] = kpt.response;
+                out[5] = __int_as_float(kpt.octave); out[6] = 0.f; out[7] = 0.f;
+            } else {
+                sb.counters[3] = 1;
+            }
+        }
+    }
+}
+
+// KeyPoint12_LessThan: x asc, y asc, size desc, angle asc, response desc, octave desc
+VO_DEV bool kp_less(const float* a, const float* b)
+{
+    if (a[0] != b[0]) return a[0] < b[0];
+    if (a[1] != b[1]) return a[1] < b[1];
+    if (a[2] != b[2]) return a[2] > b[2];
+    if (a[3] != b[3]) return a[3] < b[3];
+    if (a[4] != b[4]) return a[4] > b[4];
+    const int oa = __float_as_int(a[5]), ob = __float_as_int(b[5]);
+    if (oa != ob) return oa > ob;
+    return false;
+}
+
+#define SORT_N 16384
+__global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
+{
+    __shared__ int idx[SORT_N];
+    __shared__ int lds[16];
+    const int tid = threadIdx.x;
+    const int n = min(sb.counters[1], sb.kp_cap);
+    if (n > SORT_N) { if (tid == 0) sb.counters[3] = 1; }
+    const int nn = n < SORT_N ? n : SORT_N;
+    int P = 1;
+    while (P < nn) P <<= 1;
+    for (int i = tid; i < P; i += blockDim.x) idx[i] = i < nn ? i : -1;
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < P / 2; i += blockDim.x) {
+                const int lo = 2 * i - (i & (stride - 1));
+                const int hi = lo + stride;
+                const bool asc = ((lo & size) == 0);
+                const int a = idx[lo], c = idx[hi];
+                // "a > c" in kp_less order, padding (-1) sorts last
+                bool gt;
+                if (a < 0) gt = c >= 0;
+                else if (c < 0) gt = false;
+                else gt = kp_less(sb.kp + 8 * (int64_t)c, sb.kp + 8 * (int64_t)a);
+                if (gt == asc) { idx[lo] = c; idx[hi] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    int out = 0;
+    for (int base = 0; base < nn; base += blockDim.x) {
+        const int i = base + tid;
+        bool keep = false;
+        const float* k = nullptr;
+        if (i < nn) {
+            k = sb.kp + 8 * (int64_t)idx[i];
+            keep = true;
+            if (i > 0) {
+                const float* p = sb.kp + 8 * (int64_t)idx[i - 1];
+                keep = (k[0] != p[0] || k[1] != p[1] || k[2] != p[2] || k[3] != p[3]);
+            }
+        }
+        int tot;
+        const int pos = out + block_scan_flag(keep, lds, &tot);
+        if (keep) {
+            float* o = sb.kp_out + 6 * (int64_t)pos;
+            int oct = __float_as_int(k[5]);
+            oct = (oct & ~255) | ((oct - 1) & 255);                      // firstOctave = -1
+            o[0] = k[0] * 0.5f; o[1] = k[1] * 0.5f; o[2] = k[2] * 0.5f; o[3] = k[3]; o[4] = k[4];
+            o[5] = (float)oct;
+        }
+        out += tot;
+    }
+    if (tid == 0) sb.counters[2] = out;
+}
+
+__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= sb.counters[2]) return;
+    const float* tab = sb.consts + EXPTAB_OFF;
+    const float* kp = sb.kp_out + 6 * (int64_t)q;
+    const int kpo = (int)kp[5];
+    int octave = kpo & 255, layer = (kpo >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+    const float size = kp[2] * scale;
+    const float ptx = kp[0] * scale, pty = kp[1] * scale;
+    const int oi = octave + 1;
+    const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
+    const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
+    float angle = 360.f - kp[3];
+    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+    const float ori = angle, scl = size * 0.5f;
+    const int d = 4, n = 8;
+    const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
+    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180)));
+    float sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    const float bins_per_rad = n / 360.f;
+    const float exp_scale = -1.f / (d * d * 0.5f);
+    const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
+    int radius = __float2int_rn(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+    const int rmax = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
+    if (radius > rmax) radius = rmax;
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    float* hist = sb.hist + 360 * (int64_t)q;
+    for (int i = 0; i < (d + 2) * (d + 2) * (n + 2); ++i) hist[i] = 0.f;
+    for (int i = -radius; i <= radius; ++i) {
+        for (int j = -radius; j <= radius; ++j) {
+            const float c_rot = j * cos_t - i * sin_t;
+            const float r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + d / 2 - 0.5f;
+            float cbin = c_rot + d / 2 - 0.5f;
+            const int r = ptiy + i, c = ptix + j;
+            if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1))
+                continue;
+            const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
+            const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
+            const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
+            const float o = fast_atan2(dy, dx);
+            const float mag = sqrtf(dx * dx + dy * dy) * wgt;
+            float obin = (o - ori) * bins_per_rad;
+            int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
+            rbin -= r0; cbin -= c0; obin -= o0;
+            if (o0 < 0) o0 += n;
+            if (o0 >= n) o0 -= n;
+            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+            hist[idx] += v_rco000;
+            hist[idx + 1] += v_rco001;
+            hist[idx + (n + 2)] += v_rco010;
+            hist[idx + (n + 3)] += v_rco011;
+            hist[idx + (d + 2) * (n + 2)] += v_rco100;
+            hist[idx + (d + 2) * (n + 2) + 1] += v_rco101;
+            hist[idx + (d + 3) * (n + 2)] += v_rco110;
+            hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
+        }
+    }
+    float* dst = sb.desc + 128 * (int64_t)q;
+    for (int i = 0; i < d; ++i)
+        for (int j = 0; j < d; ++j) {
+            const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+            hist[idx] += hist[idx + n];
+            hist[idx + 1] += hist[idx + n + 1];
+            for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = hist[idx + k];
+        }
+    const int len = d * d * n;
+    float nrm2 = 0;
+    for (int k = 0; k < len; ++k) nrm2 += dst[k] * dst[k];
+    const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
+    nrm2 = 0;
+    for (int i = 0; i < len; ++i) {
+        const float v = dst[i] < thr ? dst[i] : thr;
+        dst[i] = v;
+        nrm2 += v * v;
+    }
+    const float s = sqrtf(nrm2);
+    nrm2 = SIFT_INT_DESCR_FCTR / (s > FLT_EPSILON ? s : FLT_EPSILON);
+    for (int k = 0; k < len; ++k) {
+        const int iv = __float2int_rn(dst[k] * nrm2);
+        dst[k] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
+    }
+}
+
+// ------------------------------------------------------- brute-force kNN (k = 2)
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+VO_DEV bf16x8 load_frag(const float* row, int k0, int& sq)
+{
+    const float4 a = *reinterpret_cast<const float4*>(row + k0);
+    const float4 b = *reinterpret_cast<const float4*>(row + k0 + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        f[j] = (__bf16)v[j];
+        const int iv = (int)v[j];
+        sq += iv * iv;
+    }
+    return f;
+}
+
+// one wave: 32 queries x all train rows in tiles of 32; block = 4 waves
+__global__ void __launch_bounds__(256) k_bf_knn2(const float* __restrict__ q, const int32_t* nq_p, const float* __restrict__ t,
+                                                 const int32_t* nt_p, int32_t* idx2, float* dist2)
+{
+    __shared__ float sd[4][32][33];
+    __shared__ int qn[4][32];
+    const int nq = *nq_p, nt = *nt_p;
+    const int w = wave_id(), lane = lane_id();
+    const int qbase = (blockIdx.x * 4 + w) * 32;
+    if (qbase >= nq) return;
+    const int r = lane & 31, h = lane >> 5;
+    const bool qv = qbase + r < nq;
+    const float* qrow = q + (int64_t)(qv ? qbase + r : qbase) * 128;
+    bf16x8 afr[8];
+    int sqa = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) afr[s] = load_frag(qrow, 16 * s + 8 * h, sqa);
+    sqa += __shfl_xor(sqa, 32, 64);
+    if (h == 0) qn[w][r] = qv ? sqa : 0;
+    float d0 = FLT_MAX, d1 = FLT_MAX;
+    int i0 = -1, i1 = -1;
+    for (int t0 = 0; t0 < nt; t0 += 32) {
+        const int tr = t0 + r;
+        const float* trow = t + (int64_t)(tr < nt ? tr : t0) * 128;
+        f32x16 acc = {};
+        int sqb = 0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const bf16x8 bfr = load_frag(trow, 16 * s + 8 * h, sqb);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[s], bfr, acc, 0, 0, 0);
+        }
+        sqb += __shfl_xor(sqb, 32, 64);
+        // C layout: col = lane & 31 (train), row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5) (query)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int d2 = qn[w][row] + sqb - 2 * (int)acc[reg];
+            sd[w][row][r] = sqrtf((float)d2);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        if (h == 0) {
+            const int lim = min(32, nt - t0);
+            for (int c = 0; c < lim; ++c) {
+                const float d = sd[w][r][c];
+                if (d < d1) {
+                    if (d0 > d) { d1 = d0; i1 = i0; d0 = d; i0 = t0 + c; }
+                    else { d1 = d; i1 = t0 + c; }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (h == 0 && qv) {
+        const int qi = qbase + r;
+        idx2[2 * qi] = i0; idx2[2 * qi + 1] = i1;
+        dist2[2 * qi] = d0; dist2[2 * qi + 1] = d1;
+    }
+}
+
+// ratio test + gathering (:218-245), ordered by query index
+__global__ void __launch_bounds__(256) k_ratio(const float* kp0, const float* kp1, int kps, const int32_t* idx2,
+                                              const float* dist2, const int32_t* nq_p, int qs, double ratio,
+                                              float* pts0, float* pts1, int32_t* counts, int cap)
+{
+    __shared__ int lds[16];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int nq = nq_p[b];
+    const float* k0 = kp0 + (int64_t)b * kps * 6;
+    const float* k1 = kp1 + (int64_t)b * kps * 6;
+    const int32_t* ix = idx2 + (int64_t)b * qs * 2;
+    const float* dd = dist2 + (int64_t)b * qs * 2;
+    float* a0 = pts0 + (int64_t)b * cap * 2;
+    float* a1 = pts1 + (int64_t)b * cap * 2;
+    int out = 0;
+    for (int base = 0; base < nq; base += blockDim.x) {
+        const int i = base + tid;
+        bool keep = false;
+        if (i < nq && ix[2 * i] >= 0 && ix[2 * i + 1] >= 0)
+            keep = (double)dd[2 * i] < ratio * (double)dd[2 * i + 1];
+        int tot;
+        const int pos = out + block_scan_flag(keep, lds, &tot);
+        if (keep && pos < cap) {
+            a0[2 * pos] = k0[6 * i]; a0[2 * pos + 1] = k0[6 * i + 1];
+            const int j = ix[2 * i];
+            a1[2 * pos] = k1[6 * j]; a1[2 * pos + 1] = k1[6 * j + 1];
+        }
+        out += tot;
+    }
+    if (tid == 0) counts[b] = out < cap ? out : cap;
+}
+
+}  // namespace
+
+// ======================================================================= host side
+#define VO_STREAM(s) ((hipStream_t)(s))
+static inline int hip_rc() { return hipGetLastError() == hipSuccess ? VO_OK : VO_EHIP; }
+
+extern "C" int vo_sift_plan(vo_sift_buf* sb, int W, int H)
+{
+    if (!sb || W < 1 || H < 1) return VO_EARG;
+    sb->W = W;
+    sb->H = H;
+    const int bw = 2 * W, bh = 2 * H;
+    const int mn = bw < bh ? bw : bh;
+    int n_oct = (int)lrint(log((double)mn) / log(2.) - 2) + 1;
+    if (n_oct > VO_SIFT_MAX_OCT) n_oct = VO_SIFT_MAX_OCT;
+    if (n_oct < 1) n_oct = 1;
+    sb->n_oct = n_oct;
+    int64_t go = 0, doff = 0;
+    int w = bw, h = bh;
+    for (int o = 0; o < n_oct; ++o) {
+        if (o > 0) { w = w / 2; h = h / 2; }
+        sb->oct_w[o] = w;
+        sb->oct_h[o] = h;
+        for (int i = 0; i < N_LAYERS + 3; ++i) { sb->gauss_off[o * 6 + i] = go; go += (int64_t)w * h; }
+        for (int i = 0; i < N_LAYERS + 2; ++i) { sb->dog_off[o * 5 + i] = doff; doff += (int64_t)w * h; }
+    }
+    sb->gauss_floats = go;
+    sb->dog_floats = doff;
+    sb->tmp_floats = (int64_t)bw * bh;
+    return VO_OK;
+}
+
+static int gauss_ksize(double sigma) { return ((int)lrint(sigma * 4 * 2 + 1)) | 1; }
+
+static void gauss_kernel(int n, double sigma, float* k)
+{
+    double s2 = -0.5 / (sigma * sigma), sum = 0;
+    for (int i = 0; i < n; ++i) {
+        double x = i - (n - 1) * 0.5;
+        k[i] = (float)exp(s2 * x * x);
+        sum += k[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
+}
+
+static void blur(const vo_sift_buf* sb, const float* src, float* dst, int w, int h, const float* kern_dev, int n,
+                 hipStream_t st)
+{
+    dim3 g((w + 127) / 128, h);
+    hipLaunchKernelGGL(k_blur_h, g, dim3(128), 0, st, src, sb->tmp, w, h, kern_dev, n);
+    hipLaunchKernelGGL(k_blur_v, g, dim3(128), 0, st, (const float*)sb->tmp, dst, w, h, kern_dev, n);
+}
+
+extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream)
+{
+    if (!sb || !img || sb->W != W || sb->H != H || !sb->gauss || !sb->dog || !sb->tmp || !sb->consts) return VO_EARG;
+    hipStream_t st = VO_STREAM(stream);
+    // host-side constants with the C library's exp/pow (as the oracle): kernel 0 = base blur,
+    // kernels 1..5 = layer increments, then the exp32f table
+    float consts[EXPTAB_OFF + 64];
+    memset(consts, 0, sizeof consts);
+    int ks[7];
+    const double sigma = 1.6;
+    const float sig_diff = sqrtf(fmaxf((float)(sigma * sigma) - 0.5f * 0.5f * 4, 0.01f));
+    ks[0] = gauss_ksize(sig_diff);
+    double sig[N_LAYERS + 3];
+    sig[0] = sigma;
+    const double k = pow(2., 1. / N_LAYERS);
+    for (int i = 1; i < N_LAYERS + 3; ++i) {
+        double sig_prev = pow(k, (double)(i - 1)) * sigma;
+        double sig_total = sig_prev * k;
+        sig[i] = sqrt(sig_total * sig_total - sig_prev * sig_prev);
+    }
+    for (int i = 1; i < N_LAYERS + 3; ++i) ks[i] = gauss_ksize(sig[i]);
+    for (int i = 0; i < N_LAYERS + 3; ++i)
+        if (ks[i] > KTAPS) return VO_EARG;
+    gauss_kernel(ks[0], sig_diff, consts);
+    for (int i = 1; i < N_LAYERS + 3; ++i) gauss_kernel(ks[i], sig[i], consts + i * KTAPS);
+    for (int i = 0; i < 64; ++i) consts[EXPTAB_OFF + i] = (float)(pow(2.0, i / 64.0) * EXPPOLY_32F_A0);
+    if (hipMemcpy(sb->consts, consts, sizeof consts, hipMemcpyHostToDevice) != hipSuccess) return VO_EHIP;
+    if (hipMemsetAsync(sb->counters, 0, 4 * sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
+    // base: 2x upsample + blur to sigma
+    float* g0 = sb->gauss + sb->gauss_off[0];
+    hipLaunchKernelGGL(k_upsample, dim3((2 * W + 127) / 128, 2 * H), dim3(128), 0, st, img, W, H, g0);
+    blur(sb, g0, g0, 2 * W, 2 * H, sb->consts, ks[0], st);
+    for (int o = 0; o < sb->n_oct; ++o)
+        for (int i = 0; i < N_LAYERS + 3; ++i) {
+            if (o == 0 && i == 0) continue;
+            float* dst = sb->gauss + sb->gauss_off[o * 6 + i];
+            const int w = sb->oct_w[o], h = sb->oct_h[o];
+            if (w < 1 || h < 1) continue;
+            if (i == 0) {
+                const float* src = sb->gauss + sb->gauss_off[(o - 1) * 6 + N_LAYERS];
+                hipLaunchKernelGGL(k_nn_down, dim3((w + 127) / 128, h), dim3(128), 0, st, src, sb->oct_w[o - 1],
+                                   sb->oct_h[o - 1], dst, w, h);
+            } else {
+                blur(sb, sb->gauss + sb->gauss_off[o * 6 + i - 1], dst, w, h, sb->consts + i * KTAPS, ks[i], st);
+            }
+        }
+    for (int o = 0; o < sb->n_oct; ++o)
+        for (int i = 0; i < N_LAYERS + 2; ++i) {
+            const int64_t n = (int64_t)sb->oct_w[o] * sb->oct_h[o];
+            if (n <= 0) continue;
+            hipLaunchKernelGGL(k_dog, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                               (const float*)(sb->gauss + sb->gauss_off[o * 6 + i]),
+                               (const float*)(sb->gauss + sb->gauss_off[o * 6 + i + 1]), sb->dog + sb->dog_off[o * 5 + i], n);
+        }
+    for (int o = 0; o < sb->n_oct; ++o) {
+        const int w = sb->oct_w[o], h = sb->oct_h[o];
+        if (w <= 2 * SIFT_IMG_BORDER || h <= 2 * SIFT_IMG_BORDER) continue;
+        for (int i = 1; i <= N_LAYERS; ++i)
+            hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER), dim3(128), 0,
+                               st, *sb, o, i);
+    }
+    hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
+    hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1), dim3(1024), 0, st, *sb);
+    hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64), dim3(64), 0, st, *sb);
+    return hip_rc();
+}
+
+extern "C" int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt, int32_t qcap,
+                          int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream)
+{
+    if (!q || !nq || !t || !nt || !idx2 || !dist2 || dim != 128 || qcap < 0) return VO_EARG;
+    if (qcap == 0) return VO_OK;
+    hipLaunchKernelGGL(k_bf_knn2, dim3((qcap + 127) / 128), dim3(256), 0, VO_STREAM(stream), q, nq, t, nt, idx2, dist2);
+    return hip_rc();
+}
+
+extern "C" int vo_ratio_matches(int B, const float* kp0, const float* kp1, int32_t kp_stride, const int32_t* idx2,
+                                const float* dist2, const int32_t* nq, int32_t q_stride, double ratio, float* pts0,
+                                float* pts1, int32_t* counts, int32_t cap, vo_stream_t stream)
+{
+    if (B < 1 || !kp0 || !kp1 || !idx2 || !dist2 || !nq || !pts0 || !pts1 || !counts) return VO_EARG;
+    hipLaunchKernelGGL(k_ratio, dim3(B), dim3(256), 0, VO_STREAM(stream), kp0, kp1, kp_stride, idx2, dist2, nq, q_stride,
+                       ratio, pts0, pts1, counts, cap);
+    return hip_rc();
+}

@@ -210,3 +210,138 @@ def Rodrigues(src, dst=None, jacobian=None):
     out = torch.empty(3, dtype=torch.float64, device=dev)
     L.check(L.lib().vo_rodrigues(1, 0, _p(inp), _p(out), _stream()), "vo_rodrigues")
     return out.cpu().numpy().reshape(3, 1), np.zeros((9, 3))
+
+
+# ---------------------------------------------------------------- SIFT / BF (:35-36, :226-229)
+class KeyPoint:
+    __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
+
+    def __init__(self, x=0.0, y=0.0, size=0.0, angle=-1.0, response=0.0, octave=0, class_id=-1):
+        self.pt = (float(x), float(y))
+        self.size = float(size)
+        self.angle = float(angle)
+        self.response = float(response)
+        self.octave = int(octave)
+        self.class_id = int(class_id)
+
+
+class DMatch:
+    __slots__ = ("queryIdx", "trainIdx", "imgIdx", "distance")
+
+    def __init__(self, queryIdx=-1, trainIdx=-1, imgIdx=0, distance=float(np.finfo(np.float32).max)):
+        self.queryIdx = int(queryIdx)
+        self.trainIdx = int(trainIdx)
+        self.imgIdx = int(imgIdx)
+        self.distance = float(distance)
+
+
+_SIFTS: dict = {}
+
+
+class _SIFT:
+    def detectAndCompute(self, image, mask):
+        from .features import Sift
+        if mask is not None:
+            raise NotImplementedError("mask is not used by the reference (:226 passes None)")
+        img = _gray(image)
+        H, W = img.shape
+        s = _SIFTS.get((W, H))
+        if s is None:
+            s = _SIFTS[(W, H)] = Sift(W, H, _dev())
+        s.run(torch.from_numpy(img).to(_dev()))
+        kp, desc = s.result()
+        kps = tuple(KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp)
+        return kps, (desc.copy() if len(kps) else None)
+
+
+def SIFT_create(*args, **kwargs):
+    if args or kwargs:
+        raise NotImplementedError("the reference uses the default SIFT (:35)")
+    return _SIFT()
+
+
+class _BFMatcher:
+    def knnMatch(self, queryDescriptors, trainDescriptors, k=2):
+        from .features import bf_knn2
+        if k != 2:
+            raise NotImplementedError("the reference uses k=2 (:229)")
+        q = np.ascontiguousarray(np.asarray(queryDescriptors, np.float32))
+        t = np.ascontiguousarray(np.asarray(trainDescriptors, np.float32))
+        if q.ndim != 2 or q.shape[1] != 128 or t.shape[1] != 128:
+            raise NotImplementedError("128-D float descriptors (SIFT)")
+        if not (np.array_equal(q, np.round(q)) and np.array_equal(t, np.round(t))):
+            raise NotImplementedError("the MFMA matcher is exact for integer-valued (SIFT) descriptors")
+        dev = _dev()
+        nq, nt = q.shape[0], t.shape[0]
+        if nq == 0:
+            return ()
+        dq = torch.from_numpy(q).to(dev)
+        dt = torch.from_numpy(t if nt else np.zeros((1, 128), np.float32)).to(dev)
+        cq = torch.tensor([nq], dtype=torch.int32, device=dev)
+        ct = torch.tensor([nt], dtype=torch.int32, device=dev)
+        idx2, dist2 = bf_knn2(dq, cq, dt, ct, nq)
+        idx2 = idx2.cpu().numpy()
+        dist2 = dist2.cpu().numpy()
+        out = []
+        for i in range(nq):
+            out.append(tuple(DMatch(i, int(idx2[i, j]), 0, float(dist2[i, j])) for j in range(2) if idx2[i, j] >= 0))
+        return tuple(out)
+
+
+def BFMatcher(normType=NORM_L2, crossCheck=False):
+    if normType != NORM_L2 or crossCheck:
+        raise NotImplementedError
+    return _BFMatcher()
+
+
+# ---------------------------------------------------------------- E / pose (:308, :315)
+def findEssentialMat(points1, points2, cameraMatrix, method=RANSAC, prob=0.999, threshold=1.0, maxIters=1000,
+                     mask=None):
+    if method != RANSAC:
+        raise NotImplementedError("the reference uses RANSAC (:308)")
+    p0 = np.ascontiguousarray(np.asarray(points1, np.float32).reshape(-1, 2))
+    p1 = np.ascontiguousarray(np.asarray(points2, np.float32).reshape(-1, 2))
+    n = p0.shape[0]
+    if p1.shape[0] != n:
+        raise error("points1 and points2 must have the same size")
+    o = make_opts(np.asarray(cameraMatrix, np.float64), _DEFAULT_OPTS)
+    dev = _dev()
+    a = torch.from_numpy(p0 if n else np.zeros((1, 2), np.float32)).to(dev)
+    b = torch.from_numpy(p1 if n else np.zeros((1, 2), np.float32)).to(dev)
+    cap = max(n, 1)
+    cnt = torch.tensor([n], dtype=torch.int32, device=dev)
+    E = torch.zeros(9, dtype=torch.float64, device=dev)
+    m = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = 4 * cap + 90 * 64 + 64
+    work = torch.empty(ws, dtype=torch.float64, device=dev)
+    L.check(L.lib().vo_find_essential(C.byref(o), 1, _p(a), _p(b), _p(cnt), cap, float(prob), float(threshold),
+                                      int(maxIters), _p(E), _p(m), _p(ok), _p(work), ws, _stream()),
+            "vo_find_essential")
+    mk = m.cpu().numpy()[:n].reshape(-1, 1)
+    if not int(ok.item()):
+        return None, mk
+    return E.cpu().numpy().reshape(3, 3), mk
+
+
+def recoverPose(E, points1, points2, cameraMatrix, *args, **kwargs):
+    if args or kwargs:
+        raise NotImplementedError("the reference passes (E, p0, p1, K) only (:315)")
+    p0 = np.ascontiguousarray(np.asarray(points1, np.float32).reshape(-1, 2))
+    p1 = np.ascontiguousarray(np.asarray(points2, np.float32).reshape(-1, 2))
+    n = p0.shape[0]
+    o = make_opts(np.asarray(cameraMatrix, np.float64), _DEFAULT_OPTS)
+    dev = _dev()
+    cap = max(n, 1)
+    a = torch.from_numpy(p0 if n else np.zeros((1, 2), np.float32)).to(dev)
+    b = torch.from_numpy(p1 if n else np.zeros((1, 2), np.float32)).to(dev)
+    cnt = torch.tensor([n], dtype=torch.int32, device=dev)
+    dE = torch.from_numpy(np.ascontiguousarray(np.asarray(E, np.float64).reshape(9))).to(dev)
+    R = torch.zeros(9, dtype=torch.float64, device=dev)
+    t = torch.zeros(3, dtype=torch.float64, device=dev)
+    m = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    ng = torch.zeros(1, dtype=torch.int32, device=dev)
+    L.check(L.lib().vo_recover_pose(C.byref(o), 1, _p(dE), _p(a), _p(b), _p(cnt), cap, _p(R), _p(t), _p(m), _p(ng),
+                                    _stream()), "vo_recover_pose")
+    return (int(ng.item()), R.cpu().numpy().reshape(3, 3), t.cpu().numpy().reshape(3, 1),
+            (m.cpu().numpy()[:n].reshape(-1, 1) * 255).astype(np.uint8))

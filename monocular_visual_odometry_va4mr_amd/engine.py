@@ -218,6 +218,61 @@ class Engine:
         g.replay()
         self.prev = 1 - self.prev
 
+    # ------------------------------------------------------------------ bootstrap
+    def bootstrap(self, img0, img1):
+        """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:
+        SIFT on both frames, BF 2-NN + ratio test, 5-point E-RANSAC, inlier split,
+        recoverPose, t *= sign(t_z), triangulation, pose append; then potential_frame
+        = img1 (its pyramid + derivatives become pyr[prev])."""
+        from .features import Sift, bf_knn2
+        img0 = self._frames(img0)
+        img1 = self._frames(img1)
+        d = self.dims
+        dev = self.device
+        if getattr(self, "_sift", None) is None:
+            self._sift = Sift(self.W, self.H, dev)
+        sift = self._sift
+        kcap = sift.kp_cap
+        B = self.B
+        kp0 = torch.zeros((B, kcap, 6), dtype=torch.float32, device=dev)
+        kp1 = torch.zeros_like(kp0)
+        n0 = torch.zeros(B, dtype=torch.int32, device=dev)
+        n1 = torch.zeros_like(n0)
+        idx2 = torch.full((B, kcap, 2), -1, dtype=torch.int32, device=dev)
+        dist2 = torch.zeros((B, kcap, 2), dtype=torch.float32, device=dev)
+        desc0 = torch.zeros((kcap, 128), dtype=torch.float32, device=dev)
+        for b in range(B):
+            k, dsc, n = sift.run(img0[b])
+            kp0[b].copy_(k)
+            desc0.copy_(dsc)
+            n0[b:b + 1].copy_(n)
+            overflow0 = sift.t["counters"][3].clone()
+            k, dsc, n = sift.run(img1[b])
+            kp1[b].copy_(k)
+            n1[b:b + 1].copy_(n)
+            i2, d2 = bf_knn2(desc0, n0[b:b + 1], dsc, n, kcap)
+            idx2[b].copy_(i2)
+            dist2[b].copy_(d2)
+            if int(overflow0) or sift.overflowed():
+                raise RuntimeError("SIFT capacity exceeded")
+        cap = min(d.ncap, d.pcap, kcap)
+        pts0 = torch.zeros((B, cap, 2), dtype=torch.float32, device=dev)
+        pts1 = torch.zeros_like(pts0)
+        cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        st = self.stream
+        self._chk(self.lib.vo_ratio_matches(B, C.c_void_p(kp0.data_ptr()), C.c_void_p(kp1.data_ptr()), kcap,
+                                            C.c_void_p(idx2.data_ptr()), C.c_void_p(dist2.data_ptr()),
+                                            C.c_void_p(n0.data_ptr()), kcap, float(self.opts.feature_ratio),
+                                            C.c_void_p(pts0.data_ptr()), C.c_void_p(pts1.data_ptr()),
+                                            C.c_void_p(cnt.data_ptr()), cap, st), "vo_ratio_matches")
+        self._chk(self.lib.vo_bootstrap(self._pd, self._po, self._ps, C.c_void_p(pts0.data_ptr()),
+                                        C.c_void_p(pts1.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, st),
+                  "vo_bootstrap")
+        self.prev = 0
+        self.build_pyramid(img1, self.prev, deriv=True)
+        self._boot_debug = {"kp0": kp0, "kp1": kp1, "n0": n0, "n1": n1, "idx2": idx2, "dist2": dist2,
+                            "pts0": pts0, "pts1": pts1, "cnt": cnt}
+
     # ------------------------------------------------------------------ state I/O
     def import_chain(self, b: int, *, landmarks, keypoints, cand, cand_first, cand_tau, transforms,
                      num_pts, prev_img):

@@ -1,0 +1,71 @@
+"""Device-side SIFT and brute-force matching used by the bootstrap (VisualOdometryPipeLine.py
+:209-245): ``cv2.SIFT_create().detectAndCompute`` and ``cv2.BFMatcher().knnMatch(k=2)``
+run by libvo_hip.so (csrc/vo_sift.hip).  Buffers are allocated once per image size."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+class Sift:
+    """SIFT for one image size on one device (OpenCV 4.6 defaults)."""
+
+    def __init__(self, width: int, height: int, device=None, cand_cap: int = 131072, kp_cap: int = 16384):
+        self.lib = L.lib()
+        self.device = torch.device(device or "cuda")
+        self.W, self.H = int(width), int(height)
+        sb = L.VoSiftBuf()
+        L.check(self.lib.vo_sift_plan(C.byref(sb), self.W, self.H), "vo_sift_plan")
+        dev = self.device
+        self.t = {
+            "gauss": torch.empty(sb.gauss_floats, dtype=torch.float32, device=dev),
+            "dog": torch.empty(sb.dog_floats, dtype=torch.float32, device=dev),
+            "tmp": torch.empty(sb.tmp_floats, dtype=torch.float32, device=dev),
+            "consts": torch.zeros(7 * 32 + 64, dtype=torch.float32, device=dev),
+            "counters": torch.zeros(4, dtype=torch.int32, device=dev),
+            "cand": torch.empty(cand_cap * 4, dtype=torch.int32, device=dev),
+            "kp": torch.empty(kp_cap * 8, dtype=torch.float32, device=dev),
+            "kp_out": torch.zeros(kp_cap, 6, dtype=torch.float32, device=dev),
+            "desc": torch.zeros(kp_cap, 128, dtype=torch.float32, device=dev),
+            "hist": torch.empty(kp_cap * 360, dtype=torch.float32, device=dev),
+        }
+        for k, v in self.t.items():
+            setattr(sb, k, v.data_ptr())
+        sb.cand_cap, sb.kp_cap = int(cand_cap), int(kp_cap)
+        self.sb = sb
+        self.kp_cap = int(kp_cap)
+
+    def run(self, img: torch.Tensor):
+        """Detect + describe; results stay on the device (kp_out, desc, counters[2])."""
+        if img.dtype != torch.uint8 or tuple(img.shape) != (self.H, self.W):
+            raise ValueError("SIFT input must be uint8 [H, W]")
+        img = img.to(self.device).contiguous()
+        st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        L.check(self.lib.vo_sift(C.byref(self.sb), C.c_void_p(img.data_ptr()), self.W, self.H, st), "vo_sift")
+        self._img = img      # keep alive until the stream consumes it
+        return self.t["kp_out"], self.t["desc"], self.t["counters"][2:3]
+
+    def overflowed(self) -> bool:
+        return bool(int(self.t["counters"][3]))
+
+    def result(self):
+        n = int(self.t["counters"][2])
+        if self.overflowed():
+            raise RuntimeError("SIFT capacity exceeded (raise cand_cap / kp_cap)")
+        return self.t["kp_out"][:n].cpu().numpy(), self.t["desc"][:n].cpu().numpy()
+
+
+def bf_knn2(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor, qcap: int):
+    """k=2 nearest neighbours (device counts), returns idx2 [qcap,2] i32, dist2 [qcap,2] f32."""
+    dev = q.device
+    idx2 = torch.full((qcap, 2), -1, dtype=torch.int32, device=dev)
+    dist2 = torch.full((qcap, 2), float(np.finfo(np.float32).max), dtype=torch.float32, device=dev)
+    st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    L.check(L.lib().vo_bf_knn2(C.c_void_p(q.data_ptr()), C.c_void_p(nq.data_ptr()), C.c_void_p(t.data_ptr()),
+                               C.c_void_p(nt.data_ptr()), qcap, 128, C.c_void_p(idx2.data_ptr()),
+                               C.c_void_p(dist2.data_ptr()), st), "vo_bf_knn2")
+    return idx2, dist2

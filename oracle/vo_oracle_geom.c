@@ -973,29 +973,46 @@ static const int MONO[20][3] = {
     {1, 1, 1}, {1, 1, 0}, {1, 0, 2}, {1, 0, 1}, {1, 0, 0}, {0, 1, 2}, {0, 1, 1}, {0, 1, 0},
     {0, 0, 3}, {0, 0, 2}, {0, 0, 1}, {0, 0, 0}};
 
-/* polynomial in x,y,z of degree <= 3 stored densely by exponent (a,b,c) index a*16+b*4+c */
-typedef struct { double c[64]; } poly3_t;
+/* polynomial in x,y,z of degree <= 3 stored by MONO index (20 coefficients); products
+ * accumulate term pairs in (i, j) MONO order so CPU and GPU round identically */
+typedef struct { double c[20]; } poly3_t;
+
+static int g_prod[20][20];     /* MONO index of MONO[i]*MONO[j], or -1 if degree > 3 */
+static int g_prod_init = 0;
+
+static void prod_init(void)
+{
+    if (g_prod_init) return;
+    for (int i = 0; i < 20; ++i)
+        for (int j = 0; j < 20; ++j) {
+            int a = MONO[i][0] + MONO[j][0], b = MONO[i][1] + MONO[j][1], c = MONO[i][2] + MONO[j][2];
+            g_prod[i][j] = -1;
+            if (a + b + c > 3) continue;
+            for (int k = 0; k < 20; ++k)
+                if (MONO[k][0] == a && MONO[k][1] == b && MONO[k][2] == c) g_prod[i][j] = k;
+        }
+    g_prod_init = 1;
+}
 
 static void p_zero(poly3_t* p) { memset(p, 0, sizeof *p); }
 static void p_mul(const poly3_t* a, const poly3_t* b, poly3_t* out)
 {
     poly3_t r;
     p_zero(&r);
-    for (int i = 0; i < 64; ++i) {
+    for (int i = 0; i < 20; ++i) {
         if (a->c[i] == 0.0) continue;
-        int ai = i >> 4, bi = (i >> 2) & 3, ci = i & 3;
-        for (int j = 0; j < 64; ++j) {
+        for (int j = 0; j < 20; ++j) {
             if (b->c[j] == 0.0) continue;
-            int aj = j >> 4, bj = (j >> 2) & 3, cj = j & 3;
-            if (ai + aj > 3 || bi + bj > 3 || ci + cj > 3) continue;
-            r.c[(ai + aj) * 16 + (bi + bj) * 4 + (ci + cj)] += a->c[i] * b->c[j];
+            int k = g_prod[i][j];
+            if (k < 0) continue;
+            r.c[k] += a->c[i] * b->c[j];
         }
     }
     *out = r;
 }
 static void p_axpy(double s, const poly3_t* a, poly3_t* y)
 {
-    for (int i = 0; i < 64; ++i) y->c[i] += s * a->c[i];
+    for (int i = 0; i < 20; ++i) y->c[i] += s * a->c[i];
 }
 
 /* Weierstrass / Durand-Kerner as in cv::solvePoly; c ascending (deg n), roots re/im */
@@ -1054,6 +1071,7 @@ static void null3(const double* B, double* v)
 
 int vo_o_five_point(const double* q1, const double* q2, double* E10)
 {
+    prod_init();
     /* Q (5 x 9): x2^T E x1 = 0 with e = vec(E) row-major */
     double Qt[9 * 5];   /* transpose, 9 x 5 */
     for (int i = 0; i < 5; ++i) {
@@ -1098,10 +1116,10 @@ int vo_o_five_point(const double* q1, const double* q2, double* E10)
     poly3_t Ep[9];
     for (int e = 0; e < 9; ++e) {
         p_zero(&Ep[e]);
-        Ep[e].c[1 * 16] = basis[0][e];
-        Ep[e].c[1 * 4] = basis[1][e];
-        Ep[e].c[1] = basis[2][e];
-        Ep[e].c[0] = basis[3][e];
+        Ep[e].c[12] = basis[0][e];
+        Ep[e].c[15] = basis[1][e];
+        Ep[e].c[18] = basis[2][e];
+        Ep[e].c[19] = basis[3][e];
     }
     poly3_t eqs[10];
     /* det(E) */
@@ -1154,7 +1172,7 @@ int vo_o_five_point(const double* q1, const double* q2, double* E10)
     double A[10 * 10], Bm[10 * 10];
     for (int r = 0; r < 10; ++r)
         for (int c = 0; c < 20; ++c) {
-            double v = eqs[r].c[MONO[c][0] * 16 + MONO[c][1] * 4 + MONO[c][2]];
+            double v = eqs[r].c[c];
             if (c < 10) A[r * 10 + c] = v; else Bm[r * 10 + (c - 10)] = v;
         }
     if (!gauss_solve(A, 10, Bm, 10)) return 0;
