@@ -1,0 +1,303 @@
+#!/usr/bin/env python3
+"""Benchmark of the VO per-frame hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--chains B]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (config C2, "KITTI seq00 1241x376 grayscale, full detect->KLT->PnP-RANSAC per-frame
+loop"): a seeded synthetic 1241x376 sequence of KITTI seq00's length (4541 frames, K of
+utils.py:22-24, options of main.py:20-44).  The job's N*B chains are contiguous
+subsequence shards; chain g bootstraps at frames [s_g, s_g+2] (main.py:18) and then runs
+continuous_operation (VisualOdometryPipeLine.py:326-373) on the following frames.  All
+frames are rendered into HBM before the timed region.
+
+A "step" = one continuous_operation of every chain on its rank (B frames per GPU).  Timed
+region: K steps between barrier + device synchronisation; value = frames of all ranks /
+max-over-ranks time (weak scaling: B chains per GPU whatever N is).
+
+Extra JSON fields:
+  roofline     -- the dominant stage, timed with HIP events recorded on the engine's
+                  stream around its launches inside the timed region; achieved =
+                  algorithmic bytes (DESIGN.md "Kernels") / mean stage time
+  cpu_baseline -- the CPU restatement (oracle/, OpenCV-4.6 semantics, 1 core) timed per
+                  frame on this host over a bounded sample (rank 0, N=1 only)
+  ate_vs_ref   -- ATE of the GPU trajectory vs that CPU run on the same frames
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from monocular_visual_odometry_va4mr_amd import options as Op          # noqa: E402
+from monocular_visual_odometry_va4mr_amd.engine import Engine          # noqa: E402
+from monocular_visual_odometry_va4mr_amd.synth import Renderer, poses  # noqa: E402
+from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E402
+
+SEQ_LEN = 4541          # KITTI seq00 frame count
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--chains", type=int, default=128, help="chains (shards) per GPU")
+    ap.add_argument("--preset", default="kitti")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (see profiles/)")
+    ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    return ap.parse_args()
+
+
+class StagePoses:
+    """Ground-truth poses for frames [0, n) computed once (synth.poses integrates from 0)."""
+
+    def __init__(self, n, params):
+        self.R, self.c = poses(n, params)
+
+
+def render_windows(rend, gt, starts, gap, n_after, device, chunk=64):
+    """frames[j, b] for chain b: j=0 -> s_b, j=1 -> s_b+gap, j>=2 -> s_b+gap+j-1."""
+    B = len(starts)
+    out = torch.empty((2 + n_after, B, rend.H, rend.W), dtype=torch.uint8, device=device)
+    for j in range(2 + n_after):
+        off = 0 if j == 0 else gap + j - 1
+        fidx = [s + off for s in starts]
+        for b in range(0, B, chunk):
+            f = fidx[b:b + chunk]
+            out[j, b:b + len(f)] = rend.render_batch(f, gt.R[f], gt.c[f])
+    return out
+
+
+def klt_bytes(eng, n_pts):
+    """5*sum(px) prev pyramid+derivatives + sum(px) next pyramid + 17 B/pt."""
+    d = eng.dims
+    spx = sum(d.lvl_w[i] * d.lvl_h[i] for i in range(d.nlev))
+    return 6.0 * spx * eng.B + 17.0 * n_pts
+
+
+def pyr_bytes(eng):
+    """u8 frame read + pyramid write (levels >= 1) + int16x2 derivative write, per chain."""
+    d = eng.dims
+    spx = sum(d.lvl_w[i] * d.lvl_h[i] for i in range(d.nlev))
+    return float(eng.B * (2 * eng.W * eng.H + (spx - eng.W * eng.H) + 4 * spx))
+
+
+def gftt_bytes(eng, n_corners):
+    return float(eng.B * eng.W * eng.H + 8 * n_corners)
+
+
+def cpu_baseline(K, opts, frames_np, gap):
+    """CPU restatement (oracle/, 1 thread) on one chain: bootstrap (untimed) then the
+    per-frame step; median frame time after 10 warm-up frames."""
+    from oracle import vo_pipeline_oracle as V
+    s = V.new_state(K, opts)
+    V.initialize(s, frames_np[0], frames_np[1])
+    ts = []
+    t_all = time.perf_counter()
+    for i in range(2, len(frames_np)):
+        t0 = time.perf_counter_ns()
+        V.step(s, frames_np[i])
+        ts.append((time.perf_counter_ns() - t0) * 1e-9)
+    wall = time.perf_counter() - t_all
+    med = float(np.median(ts[10:] if len(ts) > 20 else ts))
+    pos = np.array([np.asarray(t, np.float64).ravel() for _, t in s.transforms])
+    return med, wall, len(ts), pos
+
+
+def gpu_chain_positions(K, opts, frames_dev, device):
+    eng = Engine(K, opts, frames_dev.shape[-1], frames_dev.shape[-2], batch=1, device=device,
+                 ncap=16384, pcap=16384, fcap=max(64, frames_dev.shape[0] + 8))
+    eng.bootstrap(frames_dev[0:1], frames_dev[1:2])
+    for i in range(2, frames_dev.shape[0]):
+        eng.step(frames_dev[i:i + 1])
+    ex = eng.export_chain(0)
+    return np.array([np.asarray(t).ravel() for _, t in ex["transforms"]]), ex["status"]
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a ROCm GPU")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    opts, (b0, b1), _ = Op.get(args.preset)
+    gap = b1 - b0
+    B, K_steps, W_steps = args.chains, args.steps, args.warmup
+    n_after = W_steps + K_steps
+    rend = Renderer(args.preset, seed=args.seed, device=device)
+    H, Wd = rend.H, rend.W
+    Kmat = rend.K
+    n_shards = world * B
+    window = gap + 1 + n_after
+    starts_all = [min((g * SEQ_LEN) // n_shards, SEQ_LEN - window) for g in range(n_shards)]
+    starts = starts_all[rank * B:(rank + 1) * B]
+    gt = StagePoses(SEQ_LEN, rend.p)
+
+    t0 = time.perf_counter()
+    frames = render_windows(rend, gt, starts, gap, n_after, device)
+    torch.cuda.synchronize()
+    render_s = time.perf_counter() - t0
+
+    eng = Engine(Kmat, opts, Wd, H, batch=B, device=device, ncap=16384, pcap=16384, fcap=n_after + 16)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.bootstrap(frames[0], frames[1])
+    torch.cuda.synchronize()
+    boot_s = time.perf_counter() - t0
+
+    for i in range(W_steps):
+        eng.step(frames[2 + i])
+    torch.cuda.synchronize()
+
+    nst = len(Engine.STAGES)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(nst + 1)] for _ in range(K_steps)]
+
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(K_steps):
+        e = ev[k]
+        eng.step(frames[2 + W_steps + k], marks=lambda i, e=e: e[i].record())
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # per-stage HIP-event times (ms), mean over the timed steps
+    st_ms = np.zeros(nst)
+    for k in range(K_steps):
+        for i in range(nst):
+            st_ms[i] += ev[k][i].elapsed_time(ev[k][i + 1])
+    st_ms /= max(1, K_steps)
+
+    # live point counts of the last step (for the KLT algorithmic bytes)
+    npts = int((eng.t["nL"].to(torch.int64) + eng.t["nC"].to(torch.int64)).sum())
+    ncor = int(eng.t["nCorners"].to(torch.int64).sum())
+    statuses = eng.statuses()
+    n_ok = int((statuses == 0).sum())
+
+    # final pose gather to rank 0 (the one collective of the sharded path, §8e)
+    t_g = time.perf_counter()
+    packed = Sh.pack_poses(eng.t["pose_R"], eng.t["pose_t"], eng.t["nF"], eng.dims.fcap)
+    allp = Sh.gather_poses(packed)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - t_g) * 1e3
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    frames_total = world * B * K_steps
+    value = frames_total / elapsed
+    names = list(Engine.STAGES)
+    stage = {n: round(float(m), 4) for n, m in zip(names, st_ms)}
+    bytes_by = {
+        "track": klt_bytes(eng, npts),
+        "gftt": gftt_bytes(eng, ncor),
+        "pyr_build": float(eng.B * (eng.W * eng.H + sum(eng.dims.lvl_w[i] * eng.dims.lvl_h[i]
+                                                           for i in range(1, eng.dims.nlev)))),
+    }
+    # dominant HBM-class stage (pyramid/KLT/detection are judged by bytes)
+    dom = max(bytes_by, key=lambda n: st_ms[names.index(n)])
+    dom_ms = float(st_ms[names.index(dom)])
+    achieved = bytes_by[dom] / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            with open(args.traffic) as f:
+                tj = json.load(f)
+            rec = tj.get(dom)
+            if rec and int(rec.get("chains", -1)) == B:
+                traffic = float(rec["bytes_per_launch"])
+        except (OSError, ValueError, KeyError):
+            traffic = None
+    roof = {"bound": "hbm", "kernel": "vo_" + dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "algorithmic_bytes_per_launch": bytes_by[dom], "mean_ms": round(dom_ms, 4)}
+
+    out = {
+        "metric": "frames/s + ATE vs ref, KITTI seq00 1241x376 @ 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": K_steps,
+        "warmup": W_steps,
+        "ms_per_step": round(elapsed / K_steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "mixed(u8,i32,f32,f64)",
+        "data": "synthetic",
+        "config": {"workload": "C2 kitti seq00-length synthetic 1241x376, per-frame continuous_operation",
+                   "width": Wd, "height": H, "chains_per_gpu": B, "frames_per_step": world * B,
+                   "parallelism": f"shards{world}x{B}", "seq_len": SEQ_LEN, "seed": args.seed},
+        "roofline": roof,
+        "stages_ms": stage,
+        "chains_ok": n_ok,
+        "chain_status": {str(int(k)): int(v) for k, v in zip(*np.unique(statuses, return_counts=True))},
+        "points_last_step": npts,
+        "bootstrap_s": round(boot_s, 3),
+        "render_s": round(render_s, 2),
+        "gather_ms": round(gather_ms, 3),
+    }
+
+    if world == 1 and not args.no_cpu and args.cpu_frames > 2:
+        sample = render_windows(rend, gt, [0], gap, args.cpu_frames - 2, device)[:, 0]
+        fr_np = sample.cpu().numpy()
+        med, wall, n, pos_cpu = cpu_baseline(Kmat, opts, fr_np, gap)
+        out["cpu_baseline"] = {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"1 chain, {args.preset} frames 0,{gap} bootstrap + {n} steps; "
+                                         f"median step after 10 warm-up ({wall:.1f}s total)"}
+        pos_gpu, st = gpu_chain_positions(Kmat, opts, sample, device)
+        from monocular_visual_odometry_va4mr_amd.ate import ate
+        rmse, rel = ate(pos_gpu, pos_cpu)
+        out["ate_vs_ref"] = {"rmse": float(rmse), "rel_path": float(rel), "frames": int(len(pos_cpu)),
+                             "gpu_status": int(st)}
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+    if args.stages:
+        print(json.dumps({"stages_ms": stage, "bytes": bytes_by}), file=sys.stderr)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

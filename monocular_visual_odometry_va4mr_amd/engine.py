@@ -179,23 +179,37 @@ class Engine:
             raise ValueError(f"frames must be uint8 [{self.B},{self.H},{self.W}]")
         return frames.to(self.device, non_blocking=True).contiguous()
 
-    def step(self, frames):
-        """One continuous_operation for every chain (frames: uint8 [B,H,W], any device)."""
+    STAGES = ("pyr_build", "track", "pyr_deriv", "pnp", "triangulate", "gftt", "add_finish")
+
+    def step(self, frames, marks=None):
+        """One continuous_operation for every chain (frames: uint8 [B,H,W], any device).
+
+        ``marks``: optional callable invoked with the stage index before each stage and
+        with len(STAGES) after the last one (bench.py records HIP events there)."""
         frames = self._frames(frames)
-        self._step_launch(frames, self.prev)
+        self._step_launch(frames, self.prev, marks)
         self.prev = 1 - self.prev
 
-    def _step_launch(self, frames, prev):
+    def _step_launch(self, frames, prev, marks=None):
         cur = 1 - prev
         lib, st = self.lib, self.stream
         pd, po, ps = self._pd, self._po, self._ps
-        self._chk(lib.vo_pyr_build(pd, ps, cur, C.c_void_p(frames.data_ptr()), self.W * self.H, st), "vo_pyr_build")
-        self._chk(lib.vo_track(pd, po, ps, prev, st), "vo_track")
-        self._chk(lib.vo_pyr_deriv(pd, ps, cur, st), "vo_pyr_deriv")
-        self._chk(lib.vo_pnp(pd, po, ps, st), "vo_pnp")
-        self._chk(lib.vo_triangulate(pd, po, ps, 0, st), "vo_triangulate")
-        self._chk(lib.vo_gftt(pd, po, ps, cur, st), "vo_gftt")
-        self._chk(lib.vo_add_corners_finish(pd, po, ps, st), "vo_add_corners_finish")
+        fp = C.c_void_p(frames.data_ptr())
+        calls = (
+            lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, st),
+            lambda: lib.vo_track(pd, po, ps, prev, st),
+            lambda: lib.vo_pyr_deriv(pd, ps, cur, st),
+            lambda: lib.vo_pnp(pd, po, ps, st),
+            lambda: lib.vo_triangulate(pd, po, ps, 0, st),
+            lambda: lib.vo_gftt(pd, po, ps, cur, st),
+            lambda: lib.vo_add_corners_finish(pd, po, ps, st),
+        )
+        for i, (name, call) in enumerate(zip(self.STAGES, calls)):
+            if marks is not None:
+                marks(i)
+            self._chk(call(), "vo_" + name)
+        if marks is not None:
+            marks(len(calls))
 
     def capture_step(self):
         """Capture the two ping-pong variants of the step into hipGraphs; returns a

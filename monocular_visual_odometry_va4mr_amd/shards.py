@@ -1,0 +1,124 @@
+"""Subsequence sharding across chains and GPUs.
+
+The reference runs one sequence as one chain (main.py:112-124 bootstrap, :166-175 loop).
+Here a sequence is cut into contiguous shards; every shard is an independent chain that
+bootstraps at [s, s + gap] (gap = bootstrap_frames[1] - bootstrap_frames[0], main.py:18,
+48, 78) and runs continuous_operation on [s + gap + 1, e + overlap).  Shards are spread
+over ranks (one process per GPU) and over the batch dimension of each rank's Engine; the
+only collective is the final gather of per-shard poses to rank 0, which then chains the
+shards together with Sim(3) fits on the overlapping camera centres.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .ate import umeyama
+
+
+@dataclass(frozen=True)
+class Shard:
+    index: int          # global shard id
+    start: int          # first bootstrap frame
+    boot1: int          # second bootstrap frame
+    end: int            # one past the last frame processed (includes the overlap)
+
+    @property
+    def n_steps(self) -> int:
+        return max(0, self.end - self.boot1 - 1)
+
+
+def plan_shards(seq_len: int, n_shards: int, gap: int, overlap: int = 30) -> list[Shard]:
+    """Contiguous shards of [0, seq_len) with ``overlap`` frames shared by neighbours."""
+    if n_shards < 1:
+        raise ValueError("n_shards must be >= 1")
+    out = []
+    for k in range(n_shards):
+        s = (k * seq_len) // n_shards
+        e = ((k + 1) * seq_len) // n_shards
+        end = min(seq_len, e + (overlap if k + 1 < n_shards else 0))
+        if end - s < gap + 2:
+            raise ValueError(f"shard {k} too short: [{s}, {end}) with bootstrap gap {gap}")
+        out.append(Shard(k, s, s + gap, end))
+    return out
+
+
+def rank_shards(shards: list[Shard], rank: int, world: int) -> list[Shard]:
+    """Round-robin-free block assignment: rank r owns a contiguous block of shards."""
+    n = len(shards)
+    lo, hi = (rank * n) // world, ((rank + 1) * n) // world
+    return shards[lo:hi]
+
+
+def pack_poses(pose_R: torch.Tensor, pose_t: torch.Tensor, nF: torch.Tensor, fmax: int) -> torch.Tensor:
+    """[B, fmax, 13] f64: 9 rotation + 3 translation + valid flag (per chain, frame)."""
+    B = pose_R.shape[0]
+    out = torch.zeros((B, fmax, 13), dtype=torch.float64, device=pose_R.device)
+    f = min(fmax, pose_R.shape[1])
+    out[:, :f, :9] = pose_R[:, :f]
+    out[:, :f, 9:12] = pose_t[:, :f]
+    idx = torch.arange(f, device=pose_R.device)
+    out[:, :f, 12] = (idx[None, :] < nF[:, None].to(idx.device)).to(torch.float64)
+    return out
+
+
+def gather_poses(packed: torch.Tensor, group=None) -> torch.Tensor | None:
+    """All ranks contribute [B_r, fmax, 13]; rank 0 receives [sum B_r, fmax, 13].
+
+    One all_gather over the process group (RCCL on GPU tensors, gloo on CPU); ranks must
+    use equal B (the bench and the shard runner do)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return packed
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(parts, packed.contiguous(), group=group)
+    if dist.get_rank(group) != 0:
+        return None
+    return torch.cat(parts, 0)
+
+
+def unpack_centres(packed_chain: np.ndarray) -> np.ndarray:
+    """Camera centres transforms[k][1] (t_CW, as logged by main.py:172) of one chain."""
+    valid = packed_chain[:, 12] > 0.5
+    return packed_chain[valid, 9:12]
+
+
+def stitch(shards: list[Shard], centres: list[np.ndarray]) -> np.ndarray:
+    """Chain per-shard trajectories into one: shard k+1 is mapped onto shard k's frame by
+    the Sim(3) that aligns their overlapping camera centres (Umeyama), accumulated.
+
+    ``centres[k]`` holds poses for frames [boot0] + [boot1 .. end) of shard k, as in
+    transforms (index 0 = identity at the first bootstrap frame).  Returns per-frame
+    positions for frames [0, last end), NaN where no shard covers a frame."""
+    if not shards:
+        return np.zeros((0, 3))
+    total = max(s.end for s in shards)
+    out = np.full((total, 3), np.nan)
+
+    def frames_of(s: Shard):
+        return np.array([s.start] + list(range(s.boot1, s.end)))
+
+    prev_map = None     # frame -> position in the global frame for the previous shard
+    for s, c in zip(shards, centres):
+        fr = frames_of(s)[:len(c)]
+        c = np.asarray(c, np.float64)[:len(fr)]
+        if prev_map is None:
+            sc, R, t = 1.0, np.eye(3), np.zeros(3)
+        else:
+            common = [i for i, f in enumerate(fr) if f in prev_map]
+            if len(common) >= 3:
+                src = c[common]
+                dst = np.array([prev_map[fr[i]] for i in common])
+                sc, R, t = umeyama(src, dst, True)
+            else:
+                sc, R, t = 1.0, np.eye(3), np.zeros(3)
+        g = (sc * (R @ c.T)).T + t
+        prev_map = {}
+        for f, p in zip(fr, g):
+            prev_map[int(f)] = p
+            if np.isnan(out[f, 0]):
+                out[f] = p
+    return out

@@ -98,7 +98,7 @@ def poses(n_frames: int, p: SceneParams, start: int = 0):
     return np.stack(Rs), np.stack(cs)
 
 
-def _hash2(ix: torch.Tensor, iy: torch.Tensor, seed: int) -> torch.Tensor:
+def _hash2(ix: torch.Tensor, iy: torch.Tensor, seed) -> torch.Tensor:
     """Integer lattice hash -> float in [-1, 1).  int64 arithmetic, identical on CPU/GPU."""
     h = ix * 374761393 + iy * 668265263 + seed * 2147483647
     h = (h ^ (h >> 13)) * 1274126177
@@ -106,7 +106,7 @@ def _hash2(ix: torch.Tensor, iy: torch.Tensor, seed: int) -> torch.Tensor:
     return ((h & 0xFFFF).to(torch.float64) / 32768.0) - 1.0
 
 
-def _value_noise(u: torch.Tensor, v: torch.Tensor, seed: int, sharp: torch.Tensor) -> torch.Tensor:
+def _value_noise(u: torch.Tensor, v: torch.Tensor, seed, sharp: torch.Tensor) -> torch.Tensor:
     """Lattice value noise whose cell-to-cell transition is sharpened by ``sharp``
     (1 = smooth value noise, large = anti-aliased constant tiles with corners)."""
     iu = torch.floor(u)
@@ -152,14 +152,23 @@ class Renderer:
 
     @torch.no_grad()
     def render(self, frame_idx: int, R_wc: np.ndarray, c_w: np.ndarray) -> torch.Tensor:
+        return self.render_batch([frame_idx], np.asarray(R_wc)[None], np.asarray(c_w)[None])[0]
+
+    @torch.no_grad()
+    def render_batch(self, frame_idx, R_wc: np.ndarray, c_w: np.ndarray) -> torch.Tensor:
+        """Render F frames at once -> uint8 [F, H, W]; per-pixel arithmetic is identical to
+        rendering them one by one (every op is elementwise, per-frame scalars broadcast)."""
         p = self.p
         dev = self.device
-        R = [[float(R_wc[i, j]) for j in range(3)] for i in range(3)]
-        rx, ry = self.rx, self.ry
-        dx = rx * R[0][0] + ry * R[0][1] + R[0][2]
-        dy = rx * R[1][0] + ry * R[1][1] + R[1][2]
-        dz = rx * R[2][0] + ry * R[2][1] + R[2][2]
-        cx, cy, cz = float(c_w[0]), float(c_w[1]), float(c_w[2])
+        F = len(frame_idx)
+        Rt = torch.as_tensor(np.asarray(R_wc, np.float64).reshape(F, 3, 3), device=dev)
+        ct = torch.as_tensor(np.asarray(c_w, np.float64).reshape(F, 3), device=dev)
+        Rk = lambda i, j: Rt[:, i, j].view(F, 1, 1)
+        rx, ry = self.rx[None], self.ry[None]
+        dx = rx * Rk(0, 0) + ry * Rk(0, 1) + Rk(0, 2)
+        dy = rx * Rk(1, 0) + ry * Rk(1, 1) + Rk(1, 2)
+        dz = rx * Rk(2, 0) + ry * Rk(2, 1) + Rk(2, 2)
+        cx, cy, cz = (ct[:, i].view(F, 1, 1) for i in range(3))
         big = torch.full_like(dx, 1e9)
         eps = 1e-6
         # ground y = +h, ceiling y = -c, walls x = +-w
@@ -168,17 +177,21 @@ class Renderer:
         t_r = torch.where(dx > eps, (p.wall - cx) / dx.clamp(min=eps), big)
         t_l = torch.where(dx < -eps, (-p.wall - cx) / dx.clamp(max=-eps), big)
         ts = torch.stack([t_g, t_c, t_r, t_l], 0)
+        del t_g, t_c, t_r, t_l, big
         t, which = ts.min(0)
+        del ts
         px = cx + t * dx
         py = cy + t * dy
         pz = cz + t * dz
         # texture coordinates per surface
         u = torch.where(which < 2, px, pz)
         v = torch.where(which < 2, pz, py)
+        del px, py, pz
         # pixel footprint in world units, grazing-angle aware
         dnorm = torch.sqrt(dx * dx + dy * dy + dz * dz)
         cos_inc = torch.where(which < 2, dy.abs(), dx.abs()) / dnorm
         foot = t * dnorm * self.inv_f / cos_inc.clamp(min=0.03)
+        del dx, dy, dz, dnorm, cos_inc, t
         val = torch.zeros_like(u)
         amp = 1.0
         wl = p.base_wavelength
@@ -186,19 +199,18 @@ class Renderer:
         for o in range(p.octaves):
             att = ((wl / foot - 2.0) / 2.0).clamp(0.0, 1.0)
             sharp = (wl / foot / 1.5).clamp(1.0, 60.0)
-            n = torch.zeros_like(u)
-            for s in range(4):
-                m = which == s
-                if bool(m.any()):
-                    n[m] = _value_noise(u[m] / wl, v[m] / wl, int(self.seed * 131 + s * 7919 + o * 31),
-                                        sharp[m])
+            # per-surface lattice seed (seed*131 + surface*7919 + octave*31), one fused pass
+            seed_t = which.to(torch.int64) * 7919 + (self.seed * 131 + o * 31)
+            n = _value_noise(u / wl, v / wl, seed_t, sharp)
             val = val + amp * att * n
             norm += amp
             amp *= p.persistence
             wl *= 0.5
         img = p.mean + p.contrast * 2.0 * val / norm
         # sensor noise: Irwin-Hall(4) of hashed uniforms, exact integer hashing
-        base = self.pix + (self.seed * 1000003 + frame_idx) * 2654435761
+        fi = torch.as_tensor([(self.seed * 1000003 + int(f)) * 2654435761 for f in frame_idx],
+                             dtype=torch.int64, device=dev).view(F, 1, 1)
+        base = self.pix[None] + fi
         acc = torch.zeros_like(img)
         for k in range(4):
             acc = acc + (_hash2(base, torch.full_like(base, k), 17) + 1.0) * 0.5
@@ -209,8 +221,9 @@ class Renderer:
     def frames(self, n_frames: int, start: int = 0):
         Rs, cs = self.gt_poses(n_frames, start)
         out = []
-        for i in range(n_frames):
-            out.append(self.render(start + i, Rs[i], cs[i]))
+        for i in range(0, n_frames, 8):
+            j = min(n_frames, i + 8)
+            out.extend(self.render_batch(list(range(start + i, start + j)), Rs[i:j], cs[i:j]).unbind(0))
         return out, Rs, cs
 
 
