@@ -147,6 +147,11 @@ int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int fo
 /* cv2.goodFeaturesToTrack (:256) on pyramid level 0 of pyr[cur] -> state->corners. */
 int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream);
 
+/* Diagnostics: the cornerMinEigenVal / cornerHarris map goodFeaturesToTrack thresholds
+ * (featureselect.cpp), written to state->eig ([B][W*H] f32) with its max in eig_max.
+ * vo_gftt itself never stores this map. */
+int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream);
+
 /* feature_adding distance filter + append (:258-268) and the pose/num_pts append
  * (:371-373).  Call after vo_gftt. */
 int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);

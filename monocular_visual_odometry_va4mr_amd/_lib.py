@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libvo_hip.so")
+LIB_PATH = os.environ.get("VO_HIP_LIB") or os.path.join(_HERE, "_build", "libvo_hip.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 VO_MAX_LEVELS = 8
@@ -133,6 +133,7 @@ def _declare(L):
         "vo_pnp": ([D, O, S, P], C.c_int),
         "vo_triangulate": ([D, O, S, C.c_int, P], C.c_int),
         "vo_gftt": ([D, O, S, C.c_int, P], C.c_int),
+        "vo_gftt_eigmap": ([D, O, S, C.c_int, P], C.c_int),
         "vo_add_corners_finish": ([D, O, S, P], C.c_int),
         "vo_lk_points": ([D, O, S, C.c_int, P, P, i32, P, P, P, P], C.c_int),
         "vo_pnp_ransac": ([O, C.c_int, P, P, P, i32, P, P, P, P, P, P, i64, P], C.c_int),

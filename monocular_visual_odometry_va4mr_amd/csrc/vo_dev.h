@@ -32,6 +32,27 @@ VO_DEV int wave_sum_i32(int v)
     return v;
 }
 
+// Wave-wide int32 sum with DPP (VALU lane moves, no LDS crossbar): quad swaps, row
+// rotations, then the GFX9 row broadcasts; lane 63 ends with the total.
+VO_DEV int wave_sum_dpp(int x)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // row_ror:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return __builtin_amdgcn_readlane(x, 63);
+}
+
+// Exact wave-wide sum of per-lane int32 partials whose total may exceed 32 bits:
+// p = hi * 2^16 + lo with lo in [0, 65535]; both halves sum exactly in int32 over 64 lanes.
+VO_DEV int64_t wave_sum_split(int p)
+{
+    const int lo = p & 0xFFFF, hi = p >> 16;
+    return (int64_t)wave_sum_dpp(hi) * 65536 + (int64_t)wave_sum_dpp(lo);
+}
+
 // exclusive prefix of a per-thread flag over the whole block; lds must hold 16 ints
 VO_DEV int block_scan_flag(bool f, int* lds, int* total)
 {
@@ -49,6 +70,38 @@ VO_DEV int block_scan_flag(bool f, int* lds, int* total)
     __syncthreads();
     *total = tot;
     return base + pre;
+}
+
+// exclusive prefix of a per-thread count over the whole block; lds must hold 16 ints
+VO_DEV int block_scan_i32(int v, int* lds, int* total)
+{
+    const int lane = lane_id(), w = wave_id(), nw = blockDim.x >> 6;
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < nw; ++i) {
+        const int c = lds[i];
+        if (i < w) base += c;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// Linear block id -> work item such that consecutive items share an XCD: hardware
+// dispatch sends block L to XCD L % 8, so item = (L % 8) * per_xcd + L / 8 gives each
+// XCD a contiguous range (L2 locality only; results do not depend on the mapping).
+VO_DEV int xcd_item(int L, int total)
+{
+    const int per = (total + 7) >> 3;
+    return (L & 7) * per + (L >> 3);
 }
 
 // sum of an int over the block; lds must hold 16 ints

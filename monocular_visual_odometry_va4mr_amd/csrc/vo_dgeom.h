@@ -11,16 +11,24 @@
 
 namespace vg {
 
+// (small M, N only: every loop is unrolled so A, w, V live in registers; the 12x12 EPnP
+// decomposition uses svd_jacobi_wave below)
 template <int M, int N>
 VO_DEV void svd_jacobi(double* A, double* w, double* V)
 {
+    static_assert(N <= 6, "use svd_jacobi_wave for large matrices");
+#pragma unroll
     for (int i = 0; i < N; ++i)
+#pragma unroll
         for (int j = 0; j < N; ++j) V[i * N + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
         int changed = 0;
+#pragma unroll
         for (int i = 0; i < N - 1; ++i) {
+#pragma unroll
             for (int j = i + 1; j < N; ++j) {
                 double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
                 for (int k = 0; k < M; ++k) {
                     double ai = A[k * N + i], aj = A[k * N + j];
                     alpha += ai * ai;
@@ -35,11 +43,13 @@ VO_DEV void svd_jacobi(double* A, double* w, double* V)
                 if (zeta < 0) t = -t;
                 double c = 1.0 / sqrt(1.0 + t * t);
                 double s = c * t;
+#pragma unroll
                 for (int k = 0; k < M; ++k) {
                     double ai = A[k * N + i], aj = A[k * N + j];
                     A[k * N + i] = c * ai - s * aj;
                     A[k * N + j] = s * ai + c * aj;
                 }
+#pragma unroll
                 for (int k = 0; k < N; ++k) {
                     double vi = V[k * N + i], vj = V[k * N + j];
                     V[k * N + i] = c * vi - s * vj;
@@ -49,43 +59,141 @@ VO_DEV void svd_jacobi(double* A, double* w, double* V)
         }
         if (!changed) break;
     }
+#pragma unroll
     for (int i = 0; i < N; ++i) {
         double s = 0;
+#pragma unroll
         for (int k = 0; k < M; ++k) s += A[k * N + i] * A[k * N + i];
         w[i] = sqrt(s);
     }
+#pragma unroll
+    for (int i = 0; i < N - 1; ++i) {
+        // selection of the largest remaining w, then a swap, written with constant indices
+        int b = i;
+        double wb = w[i];
+#pragma unroll
+        for (int j = i + 1; j < N; ++j) if (w[j] > wb) { b = j; wb = w[j]; }
+#pragma unroll
+        for (int j = i + 1; j < N; ++j) {
+            if (b == j) {
+                double tw = w[i]; w[i] = w[j]; w[j] = tw;
+#pragma unroll
+                for (int k = 0; k < M; ++k) { double t = A[k * N + i]; A[k * N + i] = A[k * N + j]; A[k * N + j] = t; }
+#pragma unroll
+                for (int k = 0; k < N; ++k) { double t = V[k * N + i]; V[k * N + i] = V[k * N + j]; V[k * N + j] = t; }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if (w[i] > 0) {
+            double inv = 1.0 / w[i];
+#pragma unroll
+            for (int k = 0; k < M; ++k) A[k * N + i] *= inv;
+        }
+    }
+}
+
+VO_DEV void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// svd_jacobi<M, N> executed by one whole wave with A [M*N], w [N], V [N*N] in LDS
+// (row-major), M, N <= 64.  Same cyclic pair order and the same floating-point
+// operations: every lane forms the three column sums in the scalar order from
+// broadcast LDS reads (so all lanes take identical decisions), and lane k applies the
+// rotation to row k of A and V.  Bit-identical to the scalar routine.
+template <int M, int N>
+VO_DEV void svd_jacobi_wave(double* A, double* w, double* V)
+{
+    const int lane = lane_id();
+    for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        int changed = 0;
+        for (int i = 0; i < N - 1; ++i) {
+            for (int j = i + 1; j < N; ++j) {
+                double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    double ai = A[k * N + i], aj = A[k * N + j];
+                    alpha += ai * ai;
+                    beta += aj * aj;
+                    gamma += ai * aj;
+                }
+                if (alpha == 0.0 || beta == 0.0) continue;
+                if (fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
+                changed = 1;
+                double zeta = (beta - alpha) / (2.0 * gamma);
+                double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                if (zeta < 0) t = -t;
+                double c = 1.0 / sqrt(1.0 + t * t);
+                double s = c * t;
+                if (lane < M) {
+                    double ai = A[lane * N + i], aj = A[lane * N + j];
+                    A[lane * N + i] = c * ai - s * aj;
+                    A[lane * N + j] = s * ai + c * aj;
+                }
+                if (lane < N) {
+                    double vi = V[lane * N + i], vj = V[lane * N + j];
+                    V[lane * N + i] = c * vi - s * vj;
+                    V[lane * N + j] = s * vi + c * vj;
+                }
+                wave_lds_sync();
+            }
+        }
+        if (!changed) break;
+    }
+    for (int i = 0; i < N; ++i) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += A[k * N + i] * A[k * N + i];
+        if (lane == 0) w[i] = sqrt(s);
+    }
+    wave_lds_sync();
     for (int i = 0; i < N - 1; ++i) {
         int b = i;
         for (int j = i + 1; j < N; ++j) if (w[j] > w[b]) b = j;
         if (b != i) {
-            double tw = w[i]; w[i] = w[b]; w[b] = tw;
-            for (int k = 0; k < M; ++k) { double t = A[k * N + i]; A[k * N + i] = A[k * N + b]; A[k * N + b] = t; }
-            for (int k = 0; k < N; ++k) { double t = V[k * N + i]; V[k * N + i] = V[k * N + b]; V[k * N + b] = t; }
+            wave_lds_sync();
+            if (lane == 0) { double tw = w[i]; w[i] = w[b]; w[b] = tw; }
+            if (lane < M) { double t = A[lane * N + i]; A[lane * N + i] = A[lane * N + b]; A[lane * N + b] = t; }
+            if (lane < N) { double t = V[lane * N + i]; V[lane * N + i] = V[lane * N + b]; V[lane * N + b] = t; }
+            wave_lds_sync();
         }
     }
     for (int i = 0; i < N; ++i) {
         if (w[i] > 0) {
             double inv = 1.0 / w[i];
-            for (int k = 0; k < M; ++k) A[k * N + i] *= inv;
+            if (lane < M) A[lane * N + i] *= inv;
         }
     }
+    wave_lds_sync();
 }
 
 template <int M, int N>
 VO_DEV void lsq_svd(const double* A_in, const double* b, double* x)
 {
     double A[M * N], w[N], V[N * N];
+#pragma unroll
     for (int i = 0; i < M * N; ++i) A[i] = A_in[i];
     svd_jacobi<M, N>(A, w, V);
     double thr = (w[0] > 0 ? w[0] : 0) * DBL_EPSILON * (M > N ? M : N);
     double utb[N];
+#pragma unroll
     for (int i = 0; i < N; ++i) {
         double s = 0;
+#pragma unroll
         for (int k = 0; k < M; ++k) s += A[k * N + i] * b[k];
         utb[i] = (w[i] > thr) ? s / w[i] : 0.0;
     }
+#pragma unroll
     for (int j = 0; j < N; ++j) {
         double s = 0;
+#pragma unroll
         for (int i = 0; i < N; ++i) s += V[j * N + i] * utb[i];
         x[j] = s;
     }

@@ -99,10 +99,46 @@ struct LKParams {
     int ocap;
 };
 
-template <int MAXJ>
-__global__ void __launch_bounds__(256) k_lk(LKParams P)
+// Block -> (chain, point block).  With B >= 8 all blocks of one chain land on one XCD
+// (hardware dispatch is round-robin over the 8 XCDs by linear block id), so the chain's
+// pyramid level stays in that XCD's 4 MB L2 instead of being fetched by all eight.
+// The mapping only affects speed; any block order gives the same results.
+VO_DEV bool lk_block(int B, int nb, int& b, int& pb)
 {
-    const int b = blockIdx.y;
+    const int L = blockIdx.x;
+    if (B >= 8) {
+        const int xcd = L & 7, k = L >> 3;
+        b = xcd + 8 * (k / nb);
+        pb = k % nb;
+    } else {
+        b = L / nb;
+        pb = L % nb;
+    }
+    return b < B;
+}
+
+// One pyramid level of calcOpticalFlowPyrLK for every point (lkpyramid.cpp LKTrackerInvoker,
+// SURVEY.md Appendix A): levels are separate launches, coarse to fine, and the point's
+// running estimate lives in P.out between them (float, exactly as the in-register value).
+// One wave per point; the 15x15 window is spread over the lanes (MAXJ pixels per lane).
+// The next-image window moves every iteration, so each wave stages the J neighbourhood in
+// LDS as packed 2x2 pixel quads (one ds_read_b32 = the four bilinear taps) and re-stages
+// only when the estimate drifts more than M pixels.  The bilinear sum is two v_dot4_u32_u8
+// over the 14-bit weights split into 7+7 bits; all window sums are integer and exact, so
+// results match the CPU restatement bit for bit.
+#define LK_M 4
+VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
+{
+    return (uint32_t)((w00 >> shift) & mask) | ((uint32_t)((w01 >> shift) & mask) << 8) |
+           ((uint32_t)((w10 >> shift) & mask) << 16) | ((uint32_t)((w11 >> shift) & mask) << 24);
+}
+
+template <int MAXJ>
+__global__ void __launch_bounds__(256) k_lk(LKParams P, int level, int B, int nb)
+{
+    extern __shared__ uint32_t lk_tile[];
+    int b, pb;
+    if (!lk_block(B, nb, b, pb)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
     const int lane = lane_id();
     const int n0 = P.n0 ? P.n0[b] : 0;
@@ -110,29 +146,45 @@ __global__ void __launch_bounds__(256) k_lk(LKParams P)
     if (n1 <= P.seg1_min) n1 = 0;
     const int ntot = n0 + n1;
     const int ww = P.win_w, wh = P.win_h, npx = ww * wh;
+    const int TW = ww + 2 * LK_M, TH = wh + 2 * LK_M;
+    uint32_t* tile = lk_tile + wave_id() * TW * TH;
     const float hx = (ww - 1) * 0.5f, hy = (wh - 1) * 0.5f;
     const int wpb = blockDim.x >> 6;
-    for (int p = blockIdx.x * wpb + wave_id(); p < ntot; p += gridDim.x * wpb) {
+    const int cols = P.lw[level], rows = P.lh[level], pitch = P.lpitch[level];
+    const int prow = rows + 2 * VO_BORDER;
+    const uint8_t* I = P.prev + b * P.pstride + P.loff[level];
+    const int16_t* DI = P.der + b * P.dstride + 2 * P.loff[level];
+    const uint8_t* J = P.next + b * P.pstride + P.loff[level];
+    const float sc = (float)(1. / (1 << level));
+    // per-lane window slots: offsets in the level image and in the tile; slots past the
+    // window read pixel (0,0) and are zeroed through their gradients / the error mask
+    int goff[MAXJ], toff[MAXJ];
+    bool live[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int k = lane + 64 * j;
+        const int wy = k / ww, wx = k - wy * ww;
+        live[j] = k < npx;
+        goff[j] = live[j] ? wy * pitch + wx : 0;
+        toff[j] = live[j] ? wy * TW + wx : 0;
+    }
+    for (int p = pb * wpb + wave_id(); p < ntot; p += nb * wpb) {
         const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
+        const int64_t oidx = (int64_t)b * P.ocap + p;
         const float ptx = src[0], pty = src[1];
         int status = 1;
         float errv = 0.f;
-        float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
-        for (int level = P.L; level >= 0; --level) {
-            const int cols = P.lw[level], rows = P.lh[level], pitch = P.lpitch[level];
-            const uint8_t* I = P.prev + b * P.pstride + P.loff[level];
-            const int16_t* DI = P.der + b * P.dstride + 2 * P.loff[level];
-            const uint8_t* J = P.next + b * P.pstride + P.loff[level];
-            const float sc = (float)(1. / (1 << level));
-            float px = ptx * sc, py = pty * sc;
-            if (level == P.L) { ox = px; oy = py; }
-            else { ox = ox * 2.f; oy = oy * 2.f; }
-            px -= hx;
-            py -= hy;
-            const int ipx = (int)floorf(px), ipy = (int)floorf(py);
+        float px = ptx * sc, py = pty * sc;
+        float ox, oy;   // nextPts[ptidx]
+        if (level == P.L) { ox = px; oy = py; }
+        else { ox = P.out[2 * oidx] * 2.f; oy = P.out[2 * oidx + 1] * 2.f; }
+        px -= hx;
+        py -= hy;
+        const int ipx = (int)floorf(px), ipy = (int)floorf(py);
+        do {
             if (ipx < -ww || ipx >= cols || ipy < -wh || ipy >= rows) {
                 if (level == 0) { status = 0; errv = 0.f; }
-                continue;
+                break;
             }
             float a = px - ipx, bb = py - ipy;
             int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
@@ -141,41 +193,62 @@ __global__ void __launch_bounds__(256) k_lk(LKParams P)
             int iw11 = (1 << 14) - iw00 - iw01 - iw10;
             int ival[MAXJ], ixv[MAXJ], iyv[MAXJ];
             int a11 = 0, a12 = 0, a22 = 0;
+            const int64_t ib = (int64_t)(ipy + VO_BORDER) * pitch + (ipx + VO_BORDER);
 #pragma unroll
             for (int j = 0; j < MAXJ; ++j) {
-                const int k = lane + 64 * j;
-                ival[j] = 0; ixv[j] = 0; iyv[j] = 0;
-                if (k < npx) {
-                    const int wy = k / ww, wx = k - wy * ww;
-                    const int64_t o = (int64_t)(ipy + wy + VO_BORDER) * pitch + (ipx + wx + VO_BORDER);
-                    const uint8_t* s = I + o;
-                    ival[j] = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9);
-                    const int16_t* d = DI + 2 * o;
-                    const int ds = 2 * pitch;
-                    ixv[j] = DESCALE(d[0] * iw00 + d[2] * iw01 + d[ds] * iw10 + d[ds + 2] * iw11, 14);
-                    iyv[j] = DESCALE(d[1] * iw00 + d[3] * iw01 + d[ds + 1] * iw10 + d[ds + 3] * iw11, 14);
-                    a11 += ixv[j] * ixv[j];
-                    a12 += ixv[j] * iyv[j];
-                    a22 += iyv[j] * iyv[j];
-                }
+                const int64_t o = ib + goff[j];
+                const uint8_t* s = I + o;
+                const int16_t* d = DI + 2 * o;
+                const int ds = 2 * pitch;
+                const int v = DESCALE(__mul24(s[0], iw00) + __mul24(s[1], iw01) + __mul24(s[pitch], iw10) + __mul24(s[pitch + 1], iw11), 9);
+                const int gx = DESCALE(__mul24(d[0], iw00) + __mul24(d[2], iw01) + __mul24(d[ds], iw10) + __mul24(d[ds + 2], iw11), 14);
+                const int gy = DESCALE(__mul24(d[1], iw00) + __mul24(d[3], iw01) + __mul24(d[ds + 1], iw10) + __mul24(d[ds + 3], iw11), 14);
+                ival[j] = live[j] ? v : 0;
+                ixv[j] = live[j] ? gx : 0;
+                iyv[j] = live[j] ? gy : 0;
+                a11 += __mul24(ixv[j], ixv[j]);
+                a12 += __mul24(ixv[j], iyv[j]);
+                a22 += __mul24(iyv[j], iyv[j]);
             }
-            const int64_t iA11 = wave_sum_i64(a11), iA12 = wave_sum_i64(a12), iA22 = wave_sum_i64(a22);
+            const int64_t iA11 = wave_sum_split(a11), iA12 = wave_sum_split(a12), iA22 = wave_sum_split(a22);
             const float FLT_SCALE = 1.f / (1 << 20);
             const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
             float D = A11 * A22 - A12 * A12;
             const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * ww * wh);
             if (minEig < P.min_eig || D < FLT_EPSILON) {
                 if (level == 0) status = 0;
-                continue;
+                break;
             }
             D = 1.f / D;
             float nx = ox - hx, ny = oy - hy;
             float pdx = 0.f, pdy = 0.f;
+            int tx0 = -(1 << 30), ty0 = -(1 << 30);
             for (int it = 0; it < P.max_count; ++it) {
                 const int inx = (int)floorf(nx), iny = (int)floorf(ny);
                 if (inx < -ww || inx >= cols || iny < -wh || iny >= rows) {
                     if (level == 0) status = 0;
                     break;
+                }
+                if (inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) {
+                    // (re)stage the quad tile around the window; bytes outside the padded
+                    // level are never read by an in-bounds window
+                    tx0 = inx - LK_M;
+                    ty0 = iny - LK_M;
+                    __builtin_amdgcn_wave_barrier();
+                    for (int q = lane; q < TW * TH; q += 64) {
+                        const int r = q / TW, c = q - r * TW;
+                        const int gy = ty0 + r + VO_BORDER, gx = tx0 + c + VO_BORDER;
+                        uint32_t v = 0;
+                        if (gy >= 0 && gy + 1 < prow && gx >= 0 && gx + 1 < pitch) {
+                            const uint8_t* g = J + (int64_t)gy * pitch + gx;
+                            v = (uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[pitch] << 16) |
+                                ((uint32_t)g[pitch + 1] << 24);
+                        }
+                        tile[q] = v;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
                 a = nx - inx;
                 bb = ny - iny;
@@ -183,20 +256,32 @@ __global__ void __launch_bounds__(256) k_lk(LKParams P)
                 iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
                 iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
                 iw11 = (1 << 14) - iw00 - iw01 - iw10;
+                // iw00..iw10 are in [0, 2^14]; iw11 = 2^14 - (the others) can be -1, which
+                // the unsigned dot cannot take: use iw11 + 1 and subtract the tap once
+                const int neg = iw11 < 0;
+                const int w11 = iw11 + neg;
+                const uint32_t wlo = pack_w(iw00, iw01, iw10, w11, 0, 127);
+                const uint32_t whi = pack_w(iw00, iw01, iw10, w11, 7, 255);
+                const uint32_t* tb = tile + (iny - ty0) * TW + (inx - tx0);
                 int b1 = 0, b2 = 0;
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
-                    const int k = lane + 64 * j;
-                    if (k < npx) {
-                        const int wy = k / ww, wx = k - wy * ww;
-                        const uint8_t* s = J + (int64_t)(iny + wy + VO_BORDER) * pitch + (inx + wx + VO_BORDER);
-                        const int diff = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9) - ival[j];
-                        b1 += diff * ixv[j];
-                        b2 += diff * iyv[j];
-                    }
+                    const uint32_t q = tb[toff[j]];
+                    uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                                   __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                    if (neg) sum -= q >> 24;
+                    const int diff = (int)(sum >> 9) - ival[j];
+                    b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
+                    b2 += __mul24(diff, iyv[j]);
                 }
-                const float fb1 = (float)wave_sum_i64(b1) * FLT_SCALE;
-                const float fb2 = (float)wave_sum_i64(b2) * FLT_SCALE;
+                // 32-bit reductions when every partial is below 2^24 (total < 2^30)
+                const bool wide = __ballot((uint32_t)(b1 + (1 << 24)) >= (1u << 25) ||
+                                           (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
+                int64_t s1, s2;
+                if (!wide) { s1 = wave_sum_dpp(b1); s2 = wave_sum_dpp(b2); }
+                else { s1 = wave_sum_split(b1); s2 = wave_sum_split(b2); }
+                const float fb1 = (float)s1 * FLT_SCALE;
+                const float fb2 = (float)s2 * FLT_SCALE;
                 const float ddx = (A12 * fb2 - A22 * fb1) * D;
                 const float ddy = (A12 * fb1 - A11 * fb2) * D;
                 nx += ddx;
@@ -217,33 +302,31 @@ __global__ void __launch_bounds__(256) k_lk(LKParams P)
                 const int inx = (int)floorf(fx), iny = (int)floorf(fy);
                 if (inx < -ww || inx >= cols || iny < -wh || iny >= rows) {
                     status = 0;
-                    continue;
+                    break;
                 }
                 const float aa = fx - inx, cc = fy - iny;
                 iw00 = __float2int_rn((1.f - aa) * (1.f - cc) * (float)(1 << 14));
                 iw01 = __float2int_rn(aa * (1.f - cc) * (float)(1 << 14));
                 iw10 = __float2int_rn((1.f - aa) * cc * (float)(1 << 14));
                 iw11 = (1 << 14) - iw00 - iw01 - iw10;
+                const int64_t jb = (int64_t)(iny + VO_BORDER) * pitch + (inx + VO_BORDER);
                 int es = 0;
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
-                    const int k = lane + 64 * j;
-                    if (k < npx) {
-                        const int wy = k / ww, wx = k - wy * ww;
-                        const uint8_t* s = J + (int64_t)(iny + wy + VO_BORDER) * pitch + (inx + wx + VO_BORDER);
-                        const int diff = DESCALE(s[0] * iw00 + s[1] * iw01 + s[pitch] * iw10 + s[pitch + 1] * iw11, 9) - ival[j];
-                        es += diff < 0 ? -diff : diff;
-                    }
+                    const uint8_t* s = J + jb + goff[j];
+                    const int diff = DESCALE(__mul24(s[0], iw00) + __mul24(s[1], iw01) + __mul24(s[pitch], iw10) + __mul24(s[pitch + 1], iw11), 9) - ival[j];
+                    es += live[j] ? (diff < 0 ? -diff : diff) : 0;
                 }
-                errv = (float)wave_sum_i32(es) / (float)(32 * ww * wh);
+                errv = (float)wave_sum_dpp(es) / (float)(32 * ww * wh);
             }
-        }
+        } while (false);
         if (lane == 0) {
-            const int64_t o = (int64_t)b * P.ocap + p;
-            P.out[2 * o] = ox;
-            P.out[2 * o + 1] = oy;
-            P.st[o] = (uint8_t)status;
-            if (P.err) P.err[o] = errv;
+            P.out[2 * oidx] = ox;
+            P.out[2 * oidx + 1] = oy;
+            if (level == 0) {
+                P.st[oidx] = (uint8_t)status;
+                if (P.err) P.err[oidx] = errv;
+            }
         }
     }
 }
@@ -301,29 +384,55 @@ struct EigParams {
     int64_t off;
     int bs, harris;
     double harris_k;
-    float* eig;
     uint32_t* eig_max;
+    uint64_t* keys;
+    int32_t* nkeys;
+    int ccap;
+    int B, tiles_x, tiles_y;
     const int32_t* chain_status;
+    float* eig_out;          // optional [B][W*H] eigen map (diagnostics, vo_gftt_eigmap)
 };
 
-#define EIG_T 16
+// Fused cornerMinEigenVal / cornerHarris + 3x3 local-maximum test of goodFeaturesToTrack
+// (featureselect.cpp, corner.cpp) on a 64x16 output tile.
+//  * gradients: 3x3 Sobel (integer) at every covariance position, the covariance
+//    position reflected (BORDER_REFLECT_101 of boxFilter) and Sobel reading the
+//    materialised reflect-101 border of level 0;
+//  * box sums of the gradient products (integer), lambda_min in double -> float;
+//  * the eigen map is never stored: the tile recomputes a 1-pixel halo, and a pixel is a
+//    candidate iff v > 0 and v >= its 8 neighbours.  With thr = quality * max >= 0 this is
+//    exactly OpenCV's "v > thr and v == dilate(threshold(eig, thr))(x,y)"; the v > thr part
+//    needs the global max and is applied by k_gftt_select.
+//  * candidates are appended as (fkey(v) << 32 | y*W + x) with one atomic per block (the
+//    list order is irrelevant: keys are unique and k_gftt_select orders them).
+#define EIG_TW 64
+#define EIG_TH 16
 #define EIG_MAXBS 7
-__global__ void __launch_bounds__(256) k_eig(EigParams P)
+#define EIG_CW (EIG_TW + 2 + EIG_MAXBS - 1)
+#define EIG_CH (EIG_TH + 2 + EIG_MAXBS - 1)
+__global__ void __launch_bounds__(256) k_eignms(EigParams P)
 {
-    __shared__ int sdx[(EIG_T + EIG_MAXBS - 1) * (EIG_T + EIG_MAXBS - 1)];
-    __shared__ int sdy[(EIG_T + EIG_MAXBS - 1) * (EIG_T + EIG_MAXBS - 1)];
+    __shared__ int sdx[EIG_CW * EIG_CH];
+    __shared__ int sdy[EIG_CW * EIG_CH];
+    __shared__ float sE[(EIG_TH + 2) * (EIG_TW + 2)];
     __shared__ uint32_t smax;
-    const int b = blockIdx.z;
+    __shared__ int sh[16];
+    __shared__ int sbase;
+    const int ntile = P.tiles_x * P.tiles_y;
+    const int item = xcd_item(blockIdx.x, P.B * ntile);
+    if (item >= P.B * ntile) return;
+    const int b = item / ntile, t = item - b * ntile;
     if (P.chain_status && P.chain_status[b] != 0) return;
-    const int bs = P.bs, a0 = bs / 2, tw = EIG_T + bs - 1;
-    const int x0 = blockIdx.x * EIG_T, y0 = blockIdx.y * EIG_T;
+    const int ty0 = t / P.tiles_x, tx0 = t - ty0 * P.tiles_x;
+    const int x0 = tx0 * EIG_TW, y0 = ty0 * EIG_TH;
+    const int bs = P.bs, a0 = bs / 2;
+    const int ew = EIG_TW + 2, eh = EIG_TH + 2;          // eig region: tile + 1-px halo
+    const int cw = ew + bs - 1, ch = eh + bs - 1;        // covariance region
     const uint8_t* img = P.pyr + b * P.pstride + P.off;
     if (threadIdx.x == 0) smax = 0;
-    for (int q = threadIdx.x; q < tw * tw; q += blockDim.x) {
-        const int ty = q / tw, tx = q - ty * tw;
-        // box-filter taps reflect on the covariance image, then Sobel reads the
-        // reflect-101 border of the padded level-0 image
-        const int cx = refl101(x0 - a0 + tx, P.W), cy = refl101(y0 - a0 + ty, P.H);
+    for (int q = threadIdx.x; q < cw * ch; q += blockDim.x) {
+        const int qy = q / cw, qx = q - qy * cw;
+        const int cx = refl101(x0 - 1 - a0 + qx, P.W), cy = refl101(y0 - 1 - a0 + qy, P.H);
         const uint8_t* c = img + (int64_t)(cy + VO_BORDER) * P.pitch + (cx + VO_BORDER);
         const uint8_t* u = c - P.pitch;
         const uint8_t* l = c + P.pitch;
@@ -331,89 +440,86 @@ __global__ void __launch_bounds__(256) k_eig(EigParams P)
         sdy[q] = (l[-1] - u[-1]) + 2 * (l[0] - u[0]) + (l[1] - u[1]);
     }
     __syncthreads();
-    const int tx = threadIdx.x & (EIG_T - 1), ty = threadIdx.x / EIG_T;
-    const int x = x0 + tx, y = y0 + ty;
-    if (x < P.W && y < P.H) {
+    const double s = 1.0 / ((double)(1 << 2) * bs * 255.0);
+    uint32_t lmax = 0;
+    for (int e = threadIdx.x; e < ew * eh; e += blockDim.x) {
+        const int ey = e / ew, ex = e - ey * ew;
         int sxx = 0, sxy = 0, syy = 0;
         for (int i = 0; i < bs; ++i)
             for (int j = 0; j < bs; ++j) {
-                const int q = (ty + i) * tw + (tx + j);
+                const int q = (ey + i) * cw + (ex + j);
                 const int gx = sdx[q], gy = sdy[q];
                 sxx += gx * gx;
                 sxy += gx * gy;
                 syy += gy * gy;
             }
-        const double s = 1.0 / ((double)(1 << 2) * bs * 255.0);
         float v;
         if (!P.harris) {
             const int64_t T = (int64_t)sxx + syy;
             const int64_t dd = (int64_t)sxx - syy;
             const int64_t Dd = dd * dd + 4 * (int64_t)sxy * sxy;
-            const double lam = ((double)T - sqrt((double)Dd)) * (s * s * 0.5);
-            v = (float)lam;
+            v = (float)(((double)T - sqrt((double)Dd)) * (s * s * 0.5));
         } else {
             const int64_t det = (int64_t)sxx * syy - (int64_t)sxy * sxy;
             const int64_t T = (int64_t)sxx + syy;
-            const double r = ((double)det - P.harris_k * (double)(T * T)) * (s * s * s * s);
-            v = (float)r;
+            v = (float)(((double)det - P.harris_k * (double)(T * T)) * (s * s * s * s));
         }
-        P.eig[(int64_t)b * P.W * P.H + (int64_t)y * P.W + x] = v;
-        atomicMax(&smax, fkey(v));
+        sE[e] = v;
+        // the global max counts each image pixel once: the tile's own pixels only
+        const int x = x0 - 1 + ex, y = y0 - 1 + ey;
+        if (ex >= 1 && ex <= EIG_TW && ey >= 1 && ey <= EIG_TH && x < P.W && y < P.H) {
+            const uint32_t k = fkey(v);
+            lmax = k > lmax ? k : lmax;
+            if (P.eig_out) P.eig_out[(int64_t)b * P.W * P.H + (int64_t)y * P.W + x] = v;
+        }
+    }
+    // wave max, then one LDS atomic per wave
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t t2 = __shfl_xor(lmax, o, 64);
+        lmax = t2 > lmax ? t2 : lmax;
     }
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(&P.eig_max[b], smax);
-}
-
-struct NmsParams {
-    const float* eig;
-    const uint32_t* eig_max;
-    int W, H;
-    double quality;
-    uint64_t* keys;
-    int32_t* nkeys;
-    int ccap;
-    const int32_t* chain_status;
-};
-
-__global__ void __launch_bounds__(256) k_nms(NmsParams P)
-{
-    const int b = blockIdx.z;
-    if (P.chain_status && P.chain_status[b] != 0) return;
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
-    const float thr = (float)((double)fkey_inv(P.eig_max[b]) * P.quality);
-    bool cand = false;
-    uint64_t key = 0;
-    if (x >= 1 && x < P.W - 1 && y >= 1 && y < P.H - 1) {
-        const float* e = P.eig + (int64_t)b * P.W * P.H;
-        float v = e[(int64_t)y * P.W + x];
-        v = v > thr ? v : 0.f;
-        if (v != 0.f) {
-            float m = v;
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    float u = e[(int64_t)(y + dy) * P.W + (x + dx)];
-                    u = u > thr ? u : 0.f;
-                    m = u > m ? u : m;
-                }
-            if (v == m) {
-                cand = true;
-                key = ((uint64_t)fkey(v) << 32) | (uint32_t)(y * P.W + x);
+    if (lane_id() == 0 && lmax) atomicMax(&smax, lmax);
+    if (!P.keys) {
+        __syncthreads();
+        if (threadIdx.x == 0 && smax) atomicMax(&P.eig_max[b], smax);
+        return;
+    }
+    // local maxima among the tile's interior pixels (4 per thread)
+    uint64_t kk[4];
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = threadIdx.x + 256 * j;
+        const int ly = k / EIG_TW, lx = k - ly * EIG_TW;
+        const int x = x0 + lx, y = y0 + ly;
+        kk[j] = 0;
+        if (x >= 1 && x < P.W - 1 && y >= 1 && y < P.H - 1) {
+            const float* r = sE + ly * ew + lx;      // row above, centred at lx+1
+            const float v = r[ew + 1];
+            if (v > 0.f && v >= r[0] && v >= r[1] && v >= r[2] && v >= r[ew] && v >= r[ew + 2] &&
+                v >= r[2 * ew] && v >= r[2 * ew + 1] && v >= r[2 * ew + 2]) {
+                kk[j] = ((uint64_t)fkey(v) << 32) | (uint32_t)(y * P.W + x);
+                ++cnt;
             }
         }
     }
-    // wave-aggregated append (order is irrelevant: keys are unique and sorted later)
-    const unsigned long long m = __ballot(cand);
-    if (m == 0) return;
-    const int lane = lane_id();
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&P.nkeys[b], __popcll(m));
-    base = __shfl(base, leader, 64);
-    if (cand) {
-        const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (idx < P.ccap) P.keys[(int64_t)b * P.ccap + idx] = key;
+    int tot;
+    const int pre = block_scan_i32(cnt, sh, &tot);
+    if (threadIdx.x == 0) {
+        sbase = tot ? atomicAdd(&P.nkeys[b], tot) : 0;
+        if (smax) atomicMax(&P.eig_max[b], smax);
     }
+    __syncthreads();
+    int pos = sbase + pre;
+    uint64_t* out = P.keys + (int64_t)b * P.ccap;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (kk[j]) {
+            if (pos < P.ccap) out[pos] = kk[j];
+            ++pos;
+        }
 }
 
 // ---------------------------------------------------------------- GFTT selection
@@ -423,8 +529,10 @@ __global__ void __launch_bounds__(256) k_nms(NmsParams P)
 #define GRID_LDS_CELLS 22528
 
 struct SelParams {
-    const uint64_t* keys;
+    uint64_t* keys;
     const int32_t* nkeys;
+    const uint32_t* eig_max;
+    double quality;
     int ccap, W, H;
     int max_corners;
     double min_dist;
@@ -454,17 +562,32 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
     __shared__ uint32_t lgrid[GRID_LDS_CELLS];
     __shared__ uint32_t acc_xy[ACC_MAX];
     __shared__ int hist[256];
-    __shared__ int sh_int[8];
+    __shared__ int sh_int[16];
     __shared__ uint64_t sh_u64[4];
     const int b = blockIdx.x;
     if (P.chain_status[b] != 0) return;
     const int tid = threadIdx.x;
-    const int nk = P.nkeys[b];
-    if (nk > P.ccap) {
+    const int nk_all = P.nkeys[b];
+    if (nk_all > P.ccap) {
         if (tid == 0) P.chain_status[b] = VO_ST_CAPACITY;
         return;
     }
-    const uint64_t* keys = P.keys + (int64_t)b * P.ccap;
+    // quality gate of goodFeaturesToTrack: v > quality * max(eig)  (featureselect.cpp);
+    // ordered in-place compaction of the passing keys
+    uint64_t* keys = P.keys + (int64_t)b * P.ccap;
+    const float thr = (float)((double)fkey_inv(P.eig_max[b]) * P.quality);
+    const uint64_t lo = ((uint64_t)fkey(thr) + 1ull) << 32;
+    int nk = 0;
+    for (int base = 0; base < nk_all; base += blockDim.x) {
+        const int i = base + tid;
+        const uint64_t kk = i < nk_all ? keys[i] : 0ull;
+        const bool ok = i < nk_all && kk >= lo;
+        int tot;
+        const int pos = nk + block_scan_flag(ok, sh_int, &tot);
+        if (ok) keys[pos] = kk;
+        nk += tot;
+    }
+    __syncthreads();
     const double md = P.min_dist;
     const bool use_grid = md >= 1;
     const int cs = use_grid ? __double2int_rn(md) : 1;
@@ -684,10 +807,17 @@ static void fill_lk(LKParams& P, const vo_dims* d, const vo_opts* o, const vo_st
 static int launch_lk(const LKParams& P, int B, hipStream_t st)
 {
     const int npx = P.win_w * P.win_h;
-    if (P.win_w <= 2 || P.win_h <= 2 || npx > 64 * 16) return VO_EARG;
-    dim3 g(64, B);
-    if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, g, dim3(256), 0, st, P);
-    else hipLaunchKernelGGL(k_lk<16>, g, dim3(256), 0, st, P);
+    if (P.win_w <= 2 || P.win_h <= 2 || npx > 64 * 16 || B < 1) return VO_EARG;
+    // 256 blocks x 4 waves per chain: with B >= 8 one XCD (32 CUs) holds ~one chain's
+    // blocks at a time, which keeps that chain's level resident in the XCD's L2.
+    const int nb = 256;
+    const int nblk = (B >= 8 ? ((B + 7) / 8) * 8 : B) * nb;
+    const size_t lds = 4 * 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
+    if (lds > 60 * 1024) return VO_EARG;
+    for (int level = P.L; level >= 0; --level) {
+        if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(256), lds, st, P, level, B, nb);
+        else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(256), lds, st, P, level, B, nb);
+    }
     return hip_ok() ? VO_OK : VO_EHIP;
 }
 
@@ -720,6 +850,24 @@ extern "C" int vo_lk_points(const vo_dims* d, const vo_opts* o, const vo_state* 
     return launch_lk(P, d->B, VO_STREAM(stream));
 }
 
+extern "C" int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream)
+{
+    if (!d || !o || !s || cur < 0 || cur > 1) return VO_EARG;
+    if (o->feature_block_size < 1 || o->feature_block_size > EIG_MAXBS) return VO_EARG;
+    hipStream_t st = VO_STREAM(stream);
+    if (hipMemsetAsync(s->eig_max, 0, sizeof(uint32_t) * d->B, st) != hipSuccess) return VO_EHIP;
+    EigParams E;
+    E.pyr = s->pyr[cur]; E.pstride = d->pyr_stride; E.W = d->W; E.H = d->H; E.pitch = d->lvl_pitch[0];
+    E.off = d->lvl_off[0]; E.bs = o->feature_block_size; E.harris = o->feature_use_harris; E.harris_k = o->harris_k;
+    E.eig_max = s->eig_max; E.keys = nullptr; E.nkeys = nullptr; E.ccap = 0;
+    E.B = d->B; E.tiles_x = (d->W + EIG_TW - 1) / EIG_TW; E.tiles_y = (d->H + EIG_TH - 1) / EIG_TH;
+    E.chain_status = nullptr;
+    E.eig_out = s->eig;
+    const int total = d->B * E.tiles_x * E.tiles_y;
+    hipLaunchKernelGGL(k_eignms, dim3(((total + 7) / 8) * 8), dim3(256), 0, st, E);
+    return hip_ok() ? VO_OK : VO_EHIP;
+}
+
 extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream)
 {
     if (!d || !o || !s || cur < 0 || cur > 1) return VO_EARG;
@@ -730,18 +878,20 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
     EigParams E;
     E.pyr = s->pyr[cur]; E.pstride = d->pyr_stride; E.W = d->W; E.H = d->H; E.pitch = d->lvl_pitch[0];
     E.off = d->lvl_off[0]; E.bs = o->feature_block_size; E.harris = o->feature_use_harris; E.harris_k = o->harris_k;
-    E.eig = s->eig; E.eig_max = s->eig_max; E.chain_status = s->status;
-    dim3 g((d->W + EIG_T - 1) / EIG_T, (d->H + EIG_T - 1) / EIG_T, d->B);
-    hipLaunchKernelGGL(k_eig, g, dim3(256), 0, st, E);
-    NmsParams N;
-    N.eig = s->eig; N.eig_max = s->eig_max; N.W = d->W; N.H = d->H; N.quality = o->feature_quality_level;
-    N.keys = s->gf_keys; N.nkeys = s->gf_n; N.ccap = d->ccap; N.chain_status = s->status;
-    hipLaunchKernelGGL(k_nms, g, dim3(256), 0, st, N);
+    E.eig_max = s->eig_max; E.keys = s->gf_keys; E.nkeys = s->gf_n; E.ccap = d->ccap;
+    E.B = d->B; E.tiles_x = (d->W + EIG_TW - 1) / EIG_TW; E.tiles_y = (d->H + EIG_TH - 1) / EIG_TH;
+    E.chain_status = s->status;
+    E.eig_out = nullptr;
+    {
+        const int total = d->B * E.tiles_x * E.tiles_y;
+        hipLaunchKernelGGL(k_eignms, dim3(((total + 7) / 8) * 8), dim3(256), 0, st, E);
+    }
     SelParams S;
     S.keys = s->gf_keys; S.nkeys = s->gf_n; S.ccap = d->ccap; S.W = d->W; S.H = d->H;
+    S.eig_max = s->eig_max; S.quality = o->feature_quality_level;
     S.max_corners = o->feature_max_corners; S.min_dist = o->feature_min_dist;
     S.corners = s->corners; S.ncorners = s->nCorners; S.mcap = d->mcap; S.chain_status = s->status;
-    S.gscratch = (uint32_t*)s->eig;      // the eigen map is dead after NMS: reuse it as L2 grid
+    S.gscratch = (uint32_t*)s->eig;      // L2 grid when the LDS grid is too small
     S.gstride = (int64_t)d->W * d->H;
     hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), 0, st, S);
     return hip_ok() ? VO_OK : VO_EHIP;

@@ -20,6 +20,7 @@ struct EpnpShared {
     double L[60], rho[6];
     double betas[4][4], rep[4], Rs[4][9], ts[4][3];
     double tmp[80];
+    double MtM[144], dM[12];
     double pc0[3], pw0[3];
     int flip;
 };
@@ -47,35 +48,49 @@ VO_DEV void wave_det_sum(int n, F f, double* out)
     }
 }
 
-VO_DEV void qr_lsq(double* A, int m, int n, double* b, double* x)
+// Householder least squares (the oracle's qr_lsq), sizes fixed at compile time so the
+// working arrays stay in registers
+template <int M, int N>
+VO_DEV void qr_lsq(double* A, double* b, double* x)
 {
-    for (int k = 0; k < n; ++k) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
         double nrm = 0;
-        for (int i = k; i < m; ++i) nrm += A[i * n + k] * A[i * n + k];
+#pragma unroll
+        for (int i = k; i < M; ++i) nrm += A[i * N + k] * A[i * N + k];
         nrm = sqrt(nrm);
         if (nrm == 0) continue;
-        double alpha = A[k * n + k] > 0 ? -nrm : nrm;
-        double v[16];
-        for (int i = k; i < m; ++i) v[i] = A[i * n + k];
+        double alpha = A[k * N + k] > 0 ? -nrm : nrm;
+        double v[M];
+#pragma unroll
+        for (int i = k; i < M; ++i) v[i] = A[i * N + k];
         v[k] -= alpha;
         double vn = 0;
-        for (int i = k; i < m; ++i) vn += v[i] * v[i];
+#pragma unroll
+        for (int i = k; i < M; ++i) vn += v[i] * v[i];
         if (vn == 0) continue;
-        for (int j = k; j < n; ++j) {
+#pragma unroll
+        for (int j = k; j < N; ++j) {
             double s = 0;
-            for (int i = k; i < m; ++i) s += v[i] * A[i * n + j];
+#pragma unroll
+            for (int i = k; i < M; ++i) s += v[i] * A[i * N + j];
             s = 2.0 * s / vn;
-            for (int i = k; i < m; ++i) A[i * n + j] -= s * v[i];
+#pragma unroll
+            for (int i = k; i < M; ++i) A[i * N + j] -= s * v[i];
         }
         double s = 0;
-        for (int i = k; i < m; ++i) s += v[i] * b[i];
+#pragma unroll
+        for (int i = k; i < M; ++i) s += v[i] * b[i];
         s = 2.0 * s / vn;
-        for (int i = k; i < m; ++i) b[i] -= s * v[i];
+#pragma unroll
+        for (int i = k; i < M; ++i) b[i] -= s * v[i];
     }
-    for (int k = n - 1; k >= 0; --k) {
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
         double s = b[k];
-        for (int j = k + 1; j < n; ++j) s -= A[k * n + j] * x[j];
-        x[k] = (A[k * n + k] != 0) ? s / A[k * n + k] : 0.0;
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) s -= A[k * N + j] * x[j];
+        x[k] = (A[k * N + k] != 0) ? s / A[k * N + k] : 0.0;
     }
 }
 
@@ -83,6 +98,7 @@ VO_DEV void epnp_gauss_newton(const double* L, const double* rho, double* betas)
 {
     for (int it = 0; it < 5; ++it) {
         double A[24], b[6], x[4];
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double* rL = L + i * 10;
             double* rA = A + i * 4;
@@ -96,7 +112,8 @@ VO_DEV void epnp_gauss_newton(const double* L, const double* rho, double* betas)
                              rL[6] * betas[0] * betas[3] + rL[7] * betas[1] * betas[3] +
                              rL[8] * betas[2] * betas[3] + rL[9] * betas[3] * betas[3]);
         }
-        qr_lsq(A, 6, 4, b, x);
+        qr_lsq<6, 4>(A, b, x);
+#pragma unroll
         for (int i = 0; i < 4; ++i) betas[i] += x[i];
     }
 }
@@ -129,6 +146,41 @@ VO_DEV void epnp_L6x10(const double* V12, double* L)
         row[9] = DOT3(dv[3][i], dv[3][i]);
     }
 #undef DOT3
+}
+
+// Entries [Q0, Q1) of the upper triangle of M^T M (row-major a <= b), summed in the order
+// of wave_det_sum (item i -> lane i % 64, serial per lane, then the shuffle tree).
+template <int Q0, int Q1>
+VO_DEV void epnp_mtm_part(int n, const double* alphas, const double* us, double fu, double fv, double uc,
+                          double vc, double* up)
+{
+    constexpr int K = Q1 - Q0;
+    const int lane = lane_id();
+    double acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        double M1[12], M2[12];
+        const double* as = alphas + 4 * i;
+        const double u = us[2 * i], v = us[2 * i + 1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            M1[3 * k] = as[k] * fu; M1[3 * k + 1] = 0.0; M1[3 * k + 2] = as[k] * (uc - u);
+            M2[3 * k] = 0.0; M2[3 * k + 1] = as[k] * fv; M2[3 * k + 2] = as[k] * (vc - v);
+        }
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 12; ++a)
+#pragma unroll
+            for (int b = a; b < 12; ++b, ++q)
+                if (q >= Q0 && q < Q1) acc[q - Q0] += M1[a] * M1[b] + M2[a] * M2[b];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double v = acc[k];
+        for (int s = 32; s >= 1; s >>= 1) v += __shfl_down(v, s, 64);
+        if (lane == 0) up[Q0 + k] = v;
+    }
 }
 
 // compute_R_and_t for approximation `a` (all threads participate)
@@ -256,32 +308,28 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         a[0] = 1.0 - a[1] - a[2] - a[3];
     }
     __syncthreads();
-    // M^T M upper triangle (78 entries), 6 groups of 13
+    // M^T M upper triangle (78 entries): one pass over the points, 4 waves x ~20 entries
     const double fu = K[0], fv = K[4], uc = K[2], vc = K[5];
     __shared__ double up[78];
-    for (int g = 0; g < 6; ++g) {
-        if (wave_id() == 0) {
-            wave_det_sum<13>(n, [&](int i, double* c) {
-                double M1[12], M2[12];
-                const double* as = alphas + 4 * i;
-                double u = us[2 * i], v = us[2 * i + 1];
-                for (int k = 0; k < 4; ++k) {
-                    M1[3 * k] = as[k] * fu; M1[3 * k + 1] = 0.0; M1[3 * k + 2] = as[k] * (uc - u);
-                    M2[3 * k] = 0.0; M2[3 * k + 1] = as[k] * fv; M2[3 * k + 2] = as[k] * (vc - v);
-                }
-                int q = 0;
-                for (int a = 0; a < 12; ++a)
-                    for (int b = a; b < 12; ++b, ++q)
-                        if (q >= 13 * g && q < 13 * g + 13) c[q - 13 * g] = M1[a] * M1[b] + M2[a] * M2[b];
-            }, up + 13 * g);
+    switch (wave_id()) {
+        case 0: epnp_mtm_part<0, 20>(n, alphas, us, fu, fv, uc, vc, up); break;
+        case 1: epnp_mtm_part<20, 40>(n, alphas, us, fu, fv, uc, vc, up); break;
+        case 2: epnp_mtm_part<40, 60>(n, alphas, us, fu, fv, uc, vc, up); break;
+        default: epnp_mtm_part<60, 78>(n, alphas, us, fu, fv, uc, vc, up); break;
+    }
+    __syncthreads();
+    // 12x12 Jacobi SVD of M^T M by wave 0 in LDS
+    if (wave_id() == 0) {
+        for (int q = lane_id(); q < 144; q += 64) {
+            int a = q / 12, bb = q - a * 12;
+            if (a > bb) { const int t = a; a = bb; bb = t; }
+            S.MtM[q] = up[a * 12 - a * (a - 1) / 2 + (bb - a)];
         }
+        wave_lds_sync();
+        svd_jacobi_wave<12, 12>(S.MtM, S.dM, S.V12);
     }
     __syncthreads();
     if (tid == 0) {
-        double MtM[144], dM[12];
-        int q = 0;
-        for (int a = 0; a < 12; ++a) for (int b = a; b < 12; ++b) { MtM[a * 12 + b] = MtM[b * 12 + a] = up[q++]; }
-        svd_jacobi<12, 12>(MtM, dM, S.V12);
         epnp_L6x10(S.V12, S.L);
         for (int j = 0; j < 6; ++j) {
             const double* p = S.cws[PAIR_A[j]];

@@ -1,0 +1,68 @@
+"""Stage-by-stage GPU vs oracle diagnostics on golden frames (not collected by pytest).
+
+    python tests/diag_stages.py parking_c1 [first] [last]
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from conftest import golden_frames, load_golden          # noqa: E402
+from oracle import _olib as O                            # noqa: E402
+from monocular_visual_odometry_va4mr_amd import options as Op  # noqa: E402
+from monocular_visual_odometry_va4mr_amd.engine import Engine  # noqa: E402
+
+
+def main():
+    case = sys.argv[1] if len(sys.argv) > 1 else "parking_c1"
+    g = load_golden(case)
+    fr = golden_frames(g)
+    opts, boot, _ = Op.get(str(g["preset"]))
+    lo = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    hi = int(sys.argv[3]) if len(sys.argv) > 3 else min(len(fr), 25)
+    H, W = fr[0].shape
+    eng = Engine(g["K"], opts, W, H, batch=1, ncap=8192, pcap=8192, fcap=64)
+    bad = 0
+    for i in range(lo, hi - 1):
+        eng.build_pyramid(fr[i], 0, deriv=True)
+        eng.build_pyramid(fr[i + 1], 1)
+        assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+        torch.cuda.synchronize()
+        n = int(eng.t["nCorners"][0])
+        got = eng.t["corners"][0, :n].cpu().numpy()
+        ref = O.gftt(fr[i], opts["feature_max_corners"], opts["feature_quality_level"], opts["feature_min_dist"],
+                     opts["feature_block_size"])
+        g_ok = got.shape == ref.shape and np.array_equal(got, ref)
+        pts = ref.astype(np.float32)
+        npt = len(pts)
+        dpts = torch.from_numpy(pts).cuda().reshape(1, npt, 2)
+        cnt = torch.tensor([npt], dtype=torch.int32, device="cuda")
+        out = torch.zeros(1, npt, 2, device="cuda")
+        st = torch.zeros(1, npt, dtype=torch.uint8, device="cuda")
+        err = torch.zeros(1, npt, device="cuda")
+        rc = eng.lib.vo_lk_points(eng._pd, eng._po, eng._ps, 0, C.c_void_p(dpts.data_ptr()),
+                                  C.c_void_p(cnt.data_ptr()), npt, C.c_void_p(out.data_ptr()),
+                                  C.c_void_p(st.data_ptr()), C.c_void_p(err.data_ptr()), eng.stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        ro, rs, re = O.lk(fr[i], fr[i + 1], pts, tuple(opts["winSize"]), opts["maxLevel"], opts["criteria"])
+        go, gs = out.cpu().numpy()[0], st.cpu().numpy()[0]
+        lk_st = np.array_equal(gs, rs)
+        d = np.abs(go - ro).max(1)
+        lk_ok = lk_st and np.array_equal(go, ro)
+        print(f"frame {i}: gftt {'OK' if g_ok else 'DIFF'} ({len(got)} vs {len(ref)})  lk {'OK' if lk_ok else 'DIFF'} "
+              f"st_eq={lk_st} n_diff={(d > 0).sum()} max={d.max() if len(d) else 0:.3g}")
+        if not lk_ok:
+            idx = np.nonzero((d > 0) | (gs != rs))[0][:5]
+            for k in idx:
+                print("   pt", k, pts[k], "gpu", go[k], gs[k], "ref", ro[k], rs[k])
+        bad += (not g_ok) + (not lk_ok)
+    print("bad", bad)
+
+
+if __name__ == "__main__":
+    main()

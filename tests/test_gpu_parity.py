@@ -66,6 +66,8 @@ def test_gftt_bitexact(kitti_frames, engine_factory):
         got = eng.t["corners"][0, :n].cpu().numpy()
         ref = O.gftt(fr[1], mc, q, md, 3)
         assert np.array_equal(got, ref), f"GFTT q={q} md={md}: {n} vs {len(ref)}"
+        assert L.vo_gftt_eigmap(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+        torch.cuda.synchronize()
         e = eng.t["eig"][0].cpu().numpy().reshape(376, 1241)
         assert np.array_equal(e, O.eigmap(fr[1]))
 
@@ -77,7 +79,9 @@ def test_lk_bitexact(kitti_frames, engine_factory):
     pts = O.gftt(fr[0], 1400, 0.05, 7)
     rng = np.random.default_rng(0)
     extra = np.c_[rng.uniform(-30, 1270, 300), rng.uniform(-30, 400, 300)].astype(np.float32)
-    pts = np.concatenate([pts, extra])
+    # tiny sub-pixel offsets make OpenCV's iw11 = 2^14 - iw00 - iw01 - iw10 negative
+    tiny = (pts[:200] + np.float32([[1e-3, 2e-3]]) * rng.integers(1, 8, (min(200, len(pts)), 2))).astype(np.float32)
+    pts = np.concatenate([pts, extra, tiny])
     eng.build_pyramid(fr[0], 0, deriv=True)
     eng.build_pyramid(fr[1], 1)
     n = len(pts)
