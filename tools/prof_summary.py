@@ -5,7 +5,9 @@ from separate --pmc FETCH_SIZE / WRITE_SIZE passes, per-launch HBM bytes.
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE (KB) counts half the bytes of
 wide coalesced reads -> x2; WRITE_SIZE (KB) is taken as is.
 
-usage: prof_summary.py <tag> <prof_dir> [fetch_dir write_dir] [--chains B]
+usage: prof_summary.py <tag> <prof_dir> [fetch_dir write_dir] [--chains B] [--steps N]
+(--steps N = warmup + timed steps of the profiled bench run: per-stage bytes are per step,
+i.e. each kernel's mean bytes x its launches per step)
 writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_summary.md and (with PMC dirs)
 profiles/traffic.json (read by bench.py for roofline.traffic)
 """
@@ -16,7 +18,7 @@ import os
 import sys
 from collections import defaultdict
 
-STAGE_OF = {"k_lk": "track", "k_eig": "gftt", "k_nms": "gftt", "k_gftt_select": "gftt",
+STAGE_OF = {"k_lk": "track", "k_eig": "gftt", "k_nms": "gftt", "k_eignms": "gftt", "k_gftt_select": "gftt",
             "k_ingest": "pyr_build", "k_pyrdown": "pyr_build", "k_scharr": "pyr_deriv",
             "k_pnp_ransac": "pnp", "k_pnp_apply": "pnp", "k_triangulate": "triangulate",
             "k_track_compact": "track", "k_add_finish": "add_finish"}
@@ -48,9 +50,13 @@ def pmc_avg(d, counter):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     chains = None
+    nsteps = None
     if "--chains" in sys.argv:
         chains = int(sys.argv[sys.argv.index("--chains") + 1])
-        args = [a for a in args if a != str(chains)]
+    if "--steps" in sys.argv:
+        nsteps = int(sys.argv[sys.argv.index("--steps") + 1])
+    flag_vals = {sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a in ("--chains", "--steps")}
+    args = [a for a in args if a not in flag_vals]
     tag, prof = args[0], args[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out_dir = os.path.join(root, "profiles")
@@ -77,8 +83,9 @@ def main():
         if fb is not None and wb is not None and k in STAGE_OF:
             st = STAGE_OF[k]
             e = traffic.setdefault(st, {"bytes_per_launch": 0.0, "kernels": {}, "chains": chains, "tag": tag})
-            b = 2 * fb * 1024 + wb * 1024
-            e["kernels"][k] = b
+            per_step = max(1, round(int(r["Calls"]) / nsteps)) if nsteps else 1
+            b = (2 * fb * 1024 + wb * 1024) * per_step
+            e["kernels"][k] = {"bytes_per_step": b, "launches_per_step": per_step}
             e["bytes_per_launch"] += b
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
