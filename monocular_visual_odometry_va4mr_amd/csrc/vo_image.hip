@@ -127,6 +127,13 @@ VO_DEV bool lk_block(int B, int nb, int& b, int& pb)
 // over the 14-bit weights split into 7+7 bits; all window sums are integer and exact, so
 // results match the CPU restatement bit for bit.
 #define LK_M 4
+VO_DEV void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 {
     return (uint32_t)((w00 >> shift) & mask) | ((uint32_t)((w01 >> shift) & mask) << 8) |
@@ -134,7 +141,7 @@ VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 }
 
 template <int MAXJ>
-__global__ void __launch_bounds__(256) k_lk(LKParams P, int level, int B, int nb)
+__global__ void __launch_bounds__(64) k_lk(LKParams P, int level, int B, int nb)
 {
     extern __shared__ uint32_t lk_tile[];
     int b, pb;
@@ -318,6 +325,241 @@ __global__ void __launch_bounds__(256) k_lk(LKParams P, int level, int B, int nb
                     es += live[j] ? (diff < 0 ? -diff : diff) : 0;
                 }
                 errv = (float)wave_sum_dpp(es) / (float)(32 * ww * wh);
+            }
+        } while (false);
+        if (lane == 0) {
+            P.out[2 * oidx] = ox;
+            P.out[2 * oidx + 1] = oy;
+            if (level == 0) {
+                P.st[oidx] = (uint8_t)status;
+                if (P.err) P.err[oidx] = errv;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_lk_w<WW, WH>: the same LK level as k_lk for a compile-time window (the reference uses
+// 15x15 for every dataset, main.py:36,66,96), with all window data staged through LDS by
+// coalesced dword loads instead of per-lane byte gathers:
+//   IR/DR  raw rows of I (u8) and dI (int16 pairs) under the (WW+1)x(WH+1) bilinear window,
+//   JR     raw rows of J under the (TW+1)x(TH+1) tile, TW = WW + 2M,
+//   QT     the J tile as packed 2x2 quads (built from JR), read by the iterations.
+// The tile origin is clamped so every staged row lies inside the padded level; dword rows
+// may run up to 3 bytes past a row end (next row, or the >= 64-byte tail slack that the
+// caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
+// k_lk (bit-exact with the CPU restatement).
+template <int WW, int WH>
+__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int nb)
+{
+    constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
+    constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
+    constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
+    __shared__ uint32_t QT[TH * TW];
+    __shared__ uint32_t JR[(TH + 1) * JRW];
+    __shared__ uint32_t IR[(WH + 1) * IRW];
+    __shared__ uint32_t DR[(WH + 1) * DRW];
+    const uint8_t* jr8 = (const uint8_t*)JR;
+    const uint8_t* ir8 = (const uint8_t*)IR;
+    int b, pb;
+    if (!lk_block(B, nb, b, pb)) return;
+    if (P.chain_status && P.chain_status[b] != 0) return;
+    const int lane = lane_id();
+    const int n0 = P.n0 ? P.n0[b] : 0;
+    int n1 = P.n1 ? P.n1[b] : 0;
+    if (n1 <= P.seg1_min) n1 = 0;
+    const int ntot = n0 + n1;
+    const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
+    const int cols = P.lw[level], rows = P.lh[level], pitch = P.lpitch[level];
+    const uint8_t* I = P.prev + b * P.pstride + P.loff[level];
+    const int16_t* DI = P.der + b * P.dstride + 2 * P.loff[level];
+    const uint8_t* J = P.next + b * P.pstride + P.loff[level];
+    const float sc = (float)(1. / (1 << level));
+    int wyv[MAXJ], wxv[MAXJ];
+    bool live[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int k = lane + 64 * j;
+        live[j] = k < NPX;
+        wyv[j] = live[j] ? k / WW : 0;
+        wxv[j] = live[j] ? k - (k / WW) * WW : 0;
+    }
+    int tx0 = 0, ty0 = 0, jsh = 0;
+    // (re)stage the J tile so that it covers the window at (inx, iny)
+    auto stage_j = [&](int inx, int iny) {
+        tx0 = max(inx - LK_M, -VO_BORDER);
+        ty0 = min(max(iny - LK_M, -VO_BORDER), rows + VO_BORDER - 1 - TH);
+        const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
+        jsh = gx0 & 3;
+        const uint8_t* rowp = J + (int64_t)gy0 * pitch + (gx0 & ~3);
+        wave_lds_sync();
+        for (int q = lane; q < (TH + 1) * JRW; q += 64) {
+            const int r = q / JRW, c = q - r * JRW;
+            JR[q] = *(const uint32_t*)(rowp + (int64_t)r * pitch + 4 * c);
+        }
+        wave_lds_sync();
+        for (int q = lane; q < TH * TW; q += 64) {
+            const int r = q / TW, c = q - r * TW;
+            const uint8_t* s = jr8 + r * (4 * JRW) + jsh + c;
+            QT[q] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[4 * JRW] << 16) | ((uint32_t)s[4 * JRW + 1] << 24);
+        }
+        wave_lds_sync();
+    };
+    for (int p = pb + 0; p < ntot; p += nb) {
+        const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
+        const int64_t oidx = (int64_t)b * P.ocap + p;
+        const float ptx = src[0], pty = src[1];
+        int status = 1;
+        float errv = 0.f;
+        float px = ptx * sc, py = pty * sc;
+        float ox, oy;   // nextPts[ptidx]
+        if (level == P.L) { ox = px; oy = py; }
+        else { ox = P.out[2 * oidx] * 2.f; oy = P.out[2 * oidx + 1] * 2.f; }
+        px -= hx;
+        py -= hy;
+        const int ipx = (int)floorf(px), ipy = (int)floorf(py);
+        do {
+            if (ipx < -WW || ipx >= cols || ipy < -WH || ipy >= rows) {
+                if (level == 0) { status = 0; errv = 0.f; }
+                break;
+            }
+            // stage I (u8) and dI (int16 x2) rows under the window
+            {
+                const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
+                const int ish = gx & 3;
+                const uint8_t* irow = I + (int64_t)gy * pitch + (gx & ~3);
+                const uint32_t* drow = (const uint32_t*)(DI + 2 * ((int64_t)gy * pitch + gx));
+                wave_lds_sync();
+                for (int q = lane; q < (WH + 1) * IRW; q += 64) {
+                    const int r = q / IRW, c = q - r * IRW;
+                    IR[q] = *(const uint32_t*)(irow + (int64_t)r * pitch + 4 * c);
+                }
+                for (int q = lane; q < (WH + 1) * DRW; q += 64) {
+                    const int r = q / DRW, c = q - r * DRW;
+                    DR[q] = drow[(int64_t)r * pitch + c];
+                }
+                wave_lds_sync();
+                float a = px - ipx, bb = py - ipy;
+                const int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
+                const int iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
+                const int iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
+                const int iw11 = (1 << 14) - iw00 - iw01 - iw10;
+                int ival[MAXJ], ixv[MAXJ], iyv[MAXJ];
+                int a11 = 0, a12 = 0, a22 = 0;
+#pragma unroll
+                for (int j = 0; j < MAXJ; ++j) {
+                    const uint8_t* s = ir8 + wyv[j] * (4 * IRW) + ish + wxv[j];
+                    const uint32_t* d = DR + wyv[j] * DRW + wxv[j];
+                    const uint32_t d00 = d[0], d01 = d[1], d10 = d[DRW], d11 = d[DRW + 1];
+                    const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
+                                          __mul24((int)s[4 * IRW], iw10) + __mul24((int)s[4 * IRW + 1], iw11), 9);
+                    const int gx2 = DESCALE(__mul24((int)(int16_t)d00, iw00) + __mul24((int)(int16_t)d01, iw01) +
+                                            __mul24((int)(int16_t)d10, iw10) + __mul24((int)(int16_t)d11, iw11), 14);
+                    const int gy2 = DESCALE(__mul24((int)(int16_t)(d00 >> 16), iw00) + __mul24((int)(int16_t)(d01 >> 16), iw01) +
+                                            __mul24((int)(int16_t)(d10 >> 16), iw10) + __mul24((int)(int16_t)(d11 >> 16), iw11), 14);
+                    ival[j] = live[j] ? v : 0;
+                    ixv[j] = live[j] ? gx2 : 0;
+                    iyv[j] = live[j] ? gy2 : 0;
+                    a11 += __mul24(ixv[j], ixv[j]);
+                    a12 += __mul24(ixv[j], iyv[j]);
+                    a22 += __mul24(iyv[j], iyv[j]);
+                }
+                const int64_t iA11 = wave_sum_split(a11), iA12 = wave_sum_split(a12), iA22 = wave_sum_split(a22);
+                const float FLT_SCALE = 1.f / (1 << 20);
+                const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
+                float D = A11 * A22 - A12 * A12;
+                const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+                if (minEig < P.min_eig || D < FLT_EPSILON) {
+                    if (level == 0) status = 0;
+                    break;
+                }
+                D = 1.f / D;
+                float nx = ox - hx, ny = oy - hy;
+                float pdx = 0.f, pdy = 0.f;
+                bool staged = false;
+                for (int it = 0; it < P.max_count; ++it) {
+                    const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+                    if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
+                        if (level == 0) status = 0;
+                        break;
+                    }
+                    if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) {
+                        stage_j(inx, iny);
+                        staged = true;
+                    }
+                    a = nx - inx;
+                    bb = ny - iny;
+                    const int w00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
+                    const int w01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
+                    const int w10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
+                    const int w11 = (1 << 14) - w00 - w01 - w10;
+                    // iw11 can be -1: dot with w11 + 1 and subtract the tap once
+                    const int neg = w11 < 0;
+                    const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
+                    const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
+                    const uint32_t* tb = QT + (iny - ty0) * TW + (inx - tx0);
+                    int b1 = 0, b2 = 0;
+#pragma unroll
+                    for (int j = 0; j < MAXJ; ++j) {
+                        const uint32_t q = tb[wyv[j] * TW + wxv[j]];
+                        uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                                       __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                        if (neg) sum -= q >> 24;
+                        const int diff = (int)(sum >> 9) - ival[j];
+                        b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
+                        b2 += __mul24(diff, iyv[j]);
+                    }
+                    const bool wide = __ballot((uint32_t)(b1 + (1 << 24)) >= (1u << 25) ||
+                                               (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
+                    int64_t s1, s2;
+                    if (!wide) { s1 = wave_sum_dpp(b1); s2 = wave_sum_dpp(b2); }
+                    else { s1 = wave_sum_split(b1); s2 = wave_sum_split(b2); }
+                    const float fb1 = (float)s1 * FLT_SCALE;
+                    const float fb2 = (float)s2 * FLT_SCALE;
+                    const float ddx = (A12 * fb2 - A22 * fb1) * D;
+                    const float ddy = (A12 * fb1 - A11 * fb2) * D;
+                    nx += ddx;
+                    ny += ddy;
+                    ox = nx + hx;
+                    oy = ny + hy;
+                    if ((double)ddx * ddx + (double)ddy * ddy <= P.eps2) break;
+                    if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
+                        ox -= ddx * 0.5f;
+                        oy -= ddy * 0.5f;
+                        break;
+                    }
+                    pdx = ddx;
+                    pdy = ddy;
+                }
+                if (status && level == 0) {
+                    const float fx = ox - hx, fy = oy - hy;
+                    const int inx = (int)floorf(fx), iny = (int)floorf(fy);
+                    if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
+                        status = 0;
+                        break;
+                    }
+                    if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) stage_j(inx, iny);
+                    const float aa = fx - inx, cc = fy - iny;
+                    const int w00 = __float2int_rn((1.f - aa) * (1.f - cc) * (float)(1 << 14));
+                    const int w01 = __float2int_rn(aa * (1.f - cc) * (float)(1 << 14));
+                    const int w10 = __float2int_rn((1.f - aa) * cc * (float)(1 << 14));
+                    const int w11 = (1 << 14) - w00 - w01 - w10;
+                    const int neg = w11 < 0;
+                    const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
+                    const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
+                    const uint32_t* tb = QT + (iny - ty0) * TW + (inx - tx0);
+                    int es = 0;
+#pragma unroll
+                    for (int j = 0; j < MAXJ; ++j) {
+                        const uint32_t q = tb[wyv[j] * TW + wxv[j]];
+                        uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                                       __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                        if (neg) sum -= q >> 24;
+                        const int diff = (int)(sum >> 9) - ival[j];
+                        es += live[j] ? (diff < 0 ? -diff : diff) : 0;
+                    }
+                    errv = (float)wave_sum_dpp(es) / (float)(32 * WW * WH);
+                }
             }
         } while (false);
         if (lane == 0) {
@@ -530,7 +772,7 @@ __global__ void __launch_bounds__(256) k_eignms(EigParams P)
 
 struct SelParams {
     uint64_t* keys;
-    const int32_t* nkeys;
+    int32_t* nkeys;          // in: local maxima appended; out: how many passed the quality gate
     const uint32_t* eig_max;
     double quality;
     int ccap, W, H;
@@ -556,17 +798,26 @@ VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
     else atomicExch(&gg[c], v);
 }
 
+#ifdef VO_SELECT_PROF
+__device__ long long g_selprof[16];
+#define SELPROF(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_selprof[i] = wall_clock64(); } while (0)
+#else
+#define SELPROF(i) do { } while (0)
+#endif
+
 __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
 {
     __shared__ uint64_t page[PAGE];
     __shared__ uint32_t lgrid[GRID_LDS_CELLS];
     __shared__ uint32_t acc_xy[ACC_MAX];
+    __shared__ uint32_t round_xy[64];
     __shared__ int hist[256];
     __shared__ int sh_int[16];
     __shared__ uint64_t sh_u64[4];
     const int b = blockIdx.x;
     if (P.chain_status[b] != 0) return;
     const int tid = threadIdx.x;
+    SELPROF(0);
     const int nk_all = P.nkeys[b];
     if (nk_all > P.ccap) {
         if (tid == 0) P.chain_status[b] = VO_ST_CAPACITY;
@@ -588,6 +839,8 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
         nk += tot;
     }
     __syncthreads();
+    SELPROF(1);
+    if (tid == 0) P.nkeys[b] = nk;
     const double md = P.min_dist;
     const bool use_grid = md >= 1;
     const int cs = use_grid ? __double2int_rn(md) : 1;
@@ -651,6 +904,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
         __syncthreads();
         for (int i = take + tid; i < PAGE; i += blockDim.x) page[i] = 0;
         __syncthreads();
+        SELPROF(2);
         // ---- bitonic sort, descending (value desc, then larger address first)
         for (int size = 2; size <= PAGE; size <<= 1) {
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -664,7 +918,14 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                 __syncthreads();
             }
         }
-        // ---- greedy selection by wave 0, 64 candidates per round in sorted order
+        SELPROF(3);
+        // ---- greedy selection by wave 0, 64 candidates per round in sorted order.
+        // A candidate survives if no accepted corner in the 3x3 neighbouring cells is closer
+        // than minDistance (OpenCV's grid test).  Within a round, lane i additionally needs
+        // every earlier accepted lane j < i of the round to pass the same test; the lanes
+        // form a conflict mask against earlier tentative lanes, and wave-uniform scalar code
+        // walks the tentative lanes in order to pick the accepted set -- exactly OpenCV's
+        // sequential walk, without a ballot/shuffle round trip per accepted corner.
         if (wave_id() == 0) {
             const int lane = lane_id();
             for (int s0 = 0; s0 < take && nacc < limit; s0 += 64) {
@@ -693,38 +954,74 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                             }
                         }
                 }
-                while (true) {
-                    const unsigned long long m = __ballot(tent);
-                    if (m == 0 || nacc >= limit) break;
-                    const int t = __ffsll((long long)m) - 1;
-                    const int tx = __shfl(x, t, 64), ty = __shfl(y, t, 64);
-                    if (lane == t) {
-                        acc_xy[nacc] = (uint32_t)tx | ((uint32_t)ty << 16);
-                        out[2 * nacc] = (float)tx;
-                        out[2 * nacc + 1] = (float)ty;
-                        if (use_grid) {
-                            const int cell = (ty / cs) * gw + (tx / cs);
-                            const uint32_t cv = cell_get(lds, lgrid, gg, cell);
-                            uint32_t nv;
-                            if ((cv & 0xFFFFu) == 0xFFFFu) nv = (cv & 0xFFFF0000u) | (uint32_t)nacc;
-                            else nv = (cv & 0xFFFFu) | ((uint32_t)nacc << 16);
-                            cell_set(lds, lgrid, gg, cell, nv);
-                        }
-                        tent = false;
-                    }
-                    ++nacc;
-                    if (tent && use_grid && lane > t) {
-                        const int txc = tx / cs, tyc = ty / cs;
-                        if (abs(txc - xc) <= 1 && abs(tyc - yc) <= 1) {
+                const uint64_t tmask = __ballot(tent);
+                if (tmask == 0) continue;
+                uint64_t amask = tmask;
+                if (use_grid) {
+                    // conflicts with earlier tentative lanes of this round
+                    round_xy[lane] = (uint32_t)x | ((uint32_t)y << 16);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    uint32_t clo = 0, chi = 0;
+                    uint64_t rest = tmask & ((1ull << lane) - 1ull) & (tent ? ~0ull : 0ull);
+                    // uniform walk over the tentative lanes; each lane keeps the earlier ones
+                    for (uint64_t m = tmask; m; m &= m - 1) {
+                        const int j = __builtin_ctzll(m);
+                        if (!((rest >> j) & 1ull)) continue;
+                        const uint32_t a = round_xy[j];
+                        const int tx = (int)(a & 0xFFFF), ty = (int)(a >> 16);
+                        if (abs(tx / cs - xc) <= 1 && abs(ty / cs - yc) <= 1) {
                             const float ddx = (float)x - (float)tx, ddy = (float)y - (float)ty;
-                            if ((double)(ddx * ddx + ddy * ddy) < md2) tent = false;
+                            if ((double)(ddx * ddx + ddy * ddy) < md2) {
+                                if (j < 32) clo |= 1u << j; else chi |= 1u << (j - 32);
+                            }
+                        }
+                    }
+                    // in-order resolution on scalar registers
+                    amask = 0;
+                    for (uint64_t m = tmask; m; m &= m - 1) {
+                        const int j = __builtin_ctzll(m);
+                        const uint64_t cj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)clo, j) |
+                                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)chi, j) << 32);
+                        if ((cj & amask) == 0) amask |= 1ull << j;
+                    }
+                }
+                // respect maxCorners: keep the first (limit - nacc) accepted lanes
+                int nnew = __popcll(amask);
+                if (nnew > limit - nacc) {
+                    uint64_t m = amask, keep = 0;
+                    for (int c = 0; c < limit - nacc; ++c) { const uint64_t lb = m & (~m + 1ull); keep |= lb; m ^= lb; }
+                    amask = keep;
+                    nnew = limit - nacc;
+                }
+                if ((amask >> lane) & 1ull) {
+                    const int idx = nacc + __popcll(amask & ((1ull << lane) - 1ull));
+                    acc_xy[idx] = (uint32_t)x | ((uint32_t)y << 16);
+                    out[2 * idx] = (float)x;
+                    out[2 * idx + 1] = (float)y;
+                    if (use_grid) {
+                        // at most two corners share a cell; slot order inside a cell is irrelevant
+                        const int cell = yc * gw + xc;
+                        uint32_t cur = cell_get(lds, lgrid, gg, cell);
+                        for (;;) {
+                            const uint32_t nv = ((cur & 0xFFFFu) == 0xFFFFu) ? ((cur & 0xFFFF0000u) | (uint32_t)idx)
+                                                                            : ((cur & 0xFFFFu) | ((uint32_t)idx << 16));
+                            const uint32_t prev = lds ? atomicCAS(&lgrid[cell], cur, nv) : atomicCAS(&gg[cell], cur, nv);
+                            if (prev == cur) break;
+                            cur = prev;
                         }
                     }
                 }
+                nacc += nnew;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             if (lane == 0) sh_int[2] = nacc;
         }
         __syncthreads();
+        SELPROF(4);
         nacc = sh_int[2];
         upper = page[take - 1];
         has_upper = true;
@@ -808,15 +1105,23 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
 {
     const int npx = P.win_w * P.win_h;
     if (P.win_w <= 2 || P.win_h <= 2 || npx > 64 * 16 || B < 1) return VO_EARG;
-    // 256 blocks x 4 waves per chain: with B >= 8 one XCD (32 CUs) holds ~one chain's
-    // blocks at a time, which keeps that chain's level resident in the XCD's L2.
-    const int nb = 256;
+    // One wave per block (iteration counts differ wildly between points, so a wave's slot
+    // must free as soon as its own points are done), 1024 blocks per chain: with B >= 8 one
+    // XCD (32 CUs) holds about one chain at a time, which keeps that chain's level resident
+    // in the XCD's L2.
+    const int nb = 1024;
     const int nblk = (B >= 8 ? ((B + 7) / 8) * 8 : B) * nb;
-    const size_t lds = 4 * 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
+    // the LDS-staged 15x15 kernel reads whole dwords: it needs >= 64 bytes of slack after
+    // the last pyramid level
+    const int L = P.L;
+    const int64_t pyr_end = P.loff[L] + (int64_t)(P.lh[L] + 2 * VO_BORDER) * P.lpitch[L];
+    const bool staged15 = P.win_w == 15 && P.win_h == 15 && P.pstride >= pyr_end + 64;
+    const size_t lds = 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
     if (lds > 60 * 1024) return VO_EARG;
     for (int level = P.L; level >= 0; --level) {
-        if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(256), lds, st, P, level, B, nb);
-        else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(256), lds, st, P, level, B, nb);
+        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, B, nb);
+        else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
+        else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
 }

@@ -681,28 +681,42 @@ extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, 
     if (!sb || !img || sb->W != W || sb->H != H || !sb->gauss || !sb->dog || !sb->tmp || !sb->consts) return VO_EARG;
     hipStream_t st = VO_STREAM(stream);
     // host-side constants with the C library's exp/pow (as the oracle): kernel 0 = base blur,
-    // kernels 1..5 = layer increments, then the exp32f table
-    float consts[EXPTAB_OFF + 64];
-    memset(consts, 0, sizeof consts);
-    int ks[7];
-    const double sigma = 1.6;
-    const float sig_diff = sqrtf(fmaxf((float)(sigma * sigma) - 0.5f * 0.5f * 4, 0.01f));
-    ks[0] = gauss_ksize(sig_diff);
-    double sig[N_LAYERS + 3];
-    sig[0] = sigma;
-    const double k = pow(2., 1. / N_LAYERS);
-    for (int i = 1; i < N_LAYERS + 3; ++i) {
-        double sig_prev = pow(k, (double)(i - 1)) * sigma;
-        double sig_total = sig_prev * k;
-        sig[i] = sqrt(sig_total * sig_total - sig_prev * sig_prev);
-    }
-    for (int i = 1; i < N_LAYERS + 3; ++i) ks[i] = gauss_ksize(sig[i]);
-    for (int i = 0; i < N_LAYERS + 3; ++i)
-        if (ks[i] > KTAPS) return VO_EARG;
-    gauss_kernel(ks[0], sig_diff, consts);
-    for (int i = 1; i < N_LAYERS + 3; ++i) gauss_kernel(ks[i], sig[i], consts + i * KTAPS);
-    for (int i = 0; i < 64; ++i) consts[EXPTAB_OFF + i] = (float)(pow(2.0, i / 64.0) * EXPPOLY_32F_A0);
-    if (hipMemcpy(sb->consts, consts, sizeof consts, hipMemcpyHostToDevice) != hipSuccess) return VO_EHIP;
+    // kernels 1..5 = layer increments, then the exp32f table.  They depend on nothing but the
+    // SIFT defaults, so they are built once into pinned host memory (thread-safe static init)
+    // and uploaded stream-ordered: work still queued on `st` may be touching sb->consts.
+    struct SiftConsts {
+        float* host = nullptr;
+        int ks[N_LAYERS + 3];
+        bool ok = false;
+        SiftConsts()
+        {
+            if (hipHostMalloc((void**)&host, sizeof(float) * (EXPTAB_OFF + 64)) != hipSuccess) return;
+            memset(host, 0, sizeof(float) * (EXPTAB_OFF + 64));
+            const double sigma = 1.6;
+            const float sig_diff = sqrtf(fmaxf((float)(sigma * sigma) - 0.5f * 0.5f * 4, 0.01f));
+            ks[0] = gauss_ksize(sig_diff);
+            double sig[N_LAYERS + 3];
+            sig[0] = sigma;
+            const double k = pow(2., 1. / N_LAYERS);
+            for (int i = 1; i < N_LAYERS + 3; ++i) {
+                double sig_prev = pow(k, (double)(i - 1)) * sigma;
+                double sig_total = sig_prev * k;
+                sig[i] = sqrt(sig_total * sig_total - sig_prev * sig_prev);
+            }
+            for (int i = 1; i < N_LAYERS + 3; ++i) ks[i] = gauss_ksize(sig[i]);
+            for (int i = 0; i < N_LAYERS + 3; ++i)
+                if (ks[i] > KTAPS) return;
+            gauss_kernel(ks[0], sig_diff, host);
+            for (int i = 1; i < N_LAYERS + 3; ++i) gauss_kernel(ks[i], sig[i], host + i * KTAPS);
+            for (int i = 0; i < 64; ++i) host[EXPTAB_OFF + i] = (float)(pow(2.0, i / 64.0) * EXPPOLY_32F_A0);
+            ok = true;
+        }
+    };
+    static const SiftConsts SC;
+    if (!SC.ok) return VO_EHIP;
+    const int* ks = SC.ks;
+    if (hipMemcpyAsync(sb->consts, SC.host, sizeof(float) * (EXPTAB_OFF + 64), hipMemcpyHostToDevice, st) != hipSuccess)
+        return VO_EHIP;
     if (hipMemsetAsync(sb->counters, 0, 4 * sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
     // base: 2x upsample + blur to sigma
     float* g0 = sb->gauss + sb->gauss_off[0];

@@ -94,7 +94,7 @@ class Engine:
             d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv] = w, h, pitch, off
             off += (h + 2 * L.VO_BORDER) * pitch
             w, h = (w + 1) // 2, (h + 1) // 2
-        d.pyr_stride = ((off + 255) // 256) * 256
+        d.pyr_stride = ((off + 255) // 256) * 256 + 256   # tail slack for dword-row staging (k_lk_w)
         d.der_stride = 2 * d.pyr_stride
         d.ncap, d.pcap, d.fcap = int(ncap), int(pcap), int(fcap)
         d.ccap = self.W * self.H // 2 + 1024

@@ -329,6 +329,10 @@ static void free_levels(lk_level_t* lv, int L)
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
+/* iteration histogram of the LK solver loop (diagnostics for kernel design; index =
+ * iterations run at one level for one point, 0..100) */
+int vo_o_lk_iter_hist[101];
+
 int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
             const float* pts, int n, float* out_pts, uint8_t* status, float* err,
             int win_w, int win_h, int max_level, int crit_type, int max_count,
@@ -414,7 +418,9 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
             D = 1.f / D;
             nx -= hx; ny -= hy;
             float pdx = 0.f, pdy = 0.f;
+            int iters_run = 0;
             for (int j = 0; j < max_count; ++j) {
+                iters_run = j + 1;
                 int inx = (int)floorf(nx), iny = (int)floorf(ny);
                 if (inx < -win_w || inx >= cols || iny < -win_h || iny >= rows) {
                     if (level == 0) status[pi] = 0;
@@ -451,6 +457,7 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
                 }
                 pdx = ddx; pdy = ddy;
             }
+            vo_o_lk_iter_hist[iters_run]++;
             if (status[pi] && err && level == 0) {
                 float fx = out_pts[2 * pi] - hx, fy = out_pts[2 * pi + 1] - hy;
                 int inx = (int)floorf(fx), iny = (int)floorf(fy);
