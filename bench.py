@@ -53,8 +53,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=128, help="chains (shards) per GPU")
-    ap.add_argument("--groups", type=int, default=1,
+    ap.add_argument("--chains", type=int, default=384, help="chains (shards) per GPU")
+    ap.add_argument("--groups", type=int, default=2,
                     help="split the chains into this many engines, each on its own HIP stream "
                          "(latency-bound stages of one group overlap the others' kernels)")
     ap.add_argument("--preset", default="kitti")
@@ -74,16 +74,19 @@ class StagePoses:
         self.R, self.c = poses(n, params)
 
 
-def render_windows(rend, gt, starts, gap, n_after, device, chunk=64):
-    """frames[j, b] for chain b: j=0 -> s_b, j=1 -> s_b+gap, j>=2 -> s_b+gap+j-1."""
+def render_windows(rend, gt, starts, gap, n_after, device, chunk=32):
+    """frames[j, b] for chain b: j=0 -> s_b, j=1 -> s_b+gap, j>=2 -> s_b+gap+j-1.
+    Shard windows overlap, so every distinct frame is rendered once and then gathered."""
     B = len(starts)
-    out = torch.empty((2 + n_after, B, rend.H, rend.W), dtype=torch.uint8, device=device)
-    for j in range(2 + n_after):
-        off = 0 if j == 0 else gap + j - 1
-        fidx = [s + off for s in starts]
-        for b in range(0, B, chunk):
-            f = fidx[b:b + chunk]
-            out[j, b:b + len(f)] = rend.render_batch(f, gt.R[f], gt.c[f])
+    idx = np.array([[s] + [s + gap + j - 1 for j in range(1, 2 + n_after)] for s in starts]).T  # [2+n_after, B]
+    idx[1] = np.array(starts) + gap
+    uniq, inv = np.unique(idx, return_inverse=True)
+    frames_u = torch.empty((len(uniq), rend.H, rend.W), dtype=torch.uint8, device=device)
+    for i in range(0, len(uniq), chunk):
+        f = uniq[i:i + chunk]
+        frames_u[i:i + len(f)] = rend.render_batch(list(f), gt.R[f], gt.c[f])
+    out = frames_u[torch.as_tensor(inv.reshape(idx.shape), device=device)]
+    del frames_u
     return out
 
 
@@ -124,13 +127,37 @@ def cpu_baseline(K, opts, frames_np, gap):
 
 
 def gpu_chain_positions(K, opts, frames_dev, device):
+    """One chain through the engine (the drop-in class's mode): positions, final status and
+    the per-frame latency of continuous_operation (host sync after every frame)."""
     eng = Engine(K, opts, frames_dev.shape[-1], frames_dev.shape[-2], batch=1, device=device,
                  ncap=16384, pcap=16384, fcap=max(64, frames_dev.shape[0] + 8))
     eng.bootstrap(frames_dev[0:1], frames_dev[1:2])
+    torch.cuda.synchronize()
+    lat = []
     for i in range(2, frames_dev.shape[0]):
+        t0 = time.perf_counter()
         eng.step(frames_dev[i:i + 1])
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
     ex = eng.export_chain(0)
-    return np.array([np.asarray(t).ravel() for _, t in ex["transforms"]]), ex["status"]
+    pos = np.array([np.asarray(t).ravel() for _, t in ex["transforms"]])
+    med = float(np.median(lat[10:] if len(lat) > 20 else lat))
+    # the same chain again with the per-frame step replayed from a hipGraph
+    eng2 = Engine(K, opts, frames_dev.shape[-1], frames_dev.shape[-2], batch=1, device=device,
+                  ncap=16384, pcap=16384, fcap=max(64, frames_dev.shape[0] + 8))
+    eng2.bootstrap(frames_dev[0:1], frames_dev[1:2])
+    eng2.capture_step()
+    torch.cuda.synchronize()
+    lat_g = []
+    for i in range(2, frames_dev.shape[0]):
+        t0 = time.perf_counter()
+        eng2.step_graph(frames_dev[i:i + 1])
+        torch.cuda.synchronize()
+        lat_g.append(time.perf_counter() - t0)
+    pos_g = np.array([np.asarray(t).ravel() for _, t in eng2.export_chain(0)["transforms"]])
+    same = pos_g.shape == pos.shape and bool(np.array_equal(pos_g, pos))
+    med_g = float(np.median(lat_g[10:] if len(lat_g) > 20 else lat_g))
+    return pos, ex["status"], med, med_g, same
 
 
 def main():
@@ -300,18 +327,24 @@ def main():
         "gather_ms": round(gather_ms, 3),
     }
 
-    if world == 1 and not args.no_cpu and args.cpu_frames > 2:
+    if world == 1 and args.cpu_frames > 2:
         sample = render_windows(rend, gt, [0], gap, args.cpu_frames - 2, device)[:, 0]
-        fr_np = sample.cpu().numpy()
-        med, wall, n, pos_cpu = cpu_baseline(Kmat, opts, fr_np, gap)
-        out["cpu_baseline"] = {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-                               "sample": f"1 chain, {args.preset} frames 0,{gap} bootstrap + {n} steps; "
-                                         f"median step after 10 warm-up ({wall:.1f}s total)"}
-        pos_gpu, st = gpu_chain_positions(Kmat, opts, sample, device)
-        from monocular_visual_odometry_va4mr_amd.ate import ate
-        rmse, rel = ate(pos_gpu, pos_cpu)
-        out["ate_vs_ref"] = {"rmse": float(rmse), "rel_path": float(rel), "frames": int(len(pos_cpu)),
-                             "gpu_status": int(st)}
+        pos_gpu, st, lat, lat_g, same = gpu_chain_positions(Kmat, opts, sample, device)
+        out["single_chain"] = {"frames_per_s": round(1.0 / lat, 1), "ms_per_frame": round(lat * 1e3, 3),
+                               "graph_frames_per_s": round(1.0 / lat_g, 1), "graph_identical": same,
+                               "note": "one chain (drop-in VisualOdometryPipeLine mode), host sync per frame"}
+        if not args.no_cpu:
+            fr_np = sample.cpu().numpy()
+            med, wall, n, pos_cpu = cpu_baseline(Kmat, opts, fr_np, gap)
+            out["cpu_baseline"] = {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+                                   "sample": f"1 chain, {args.preset} frames 0,{gap} bootstrap + {n} steps; "
+                                             f"median step after 10 warm-up ({wall:.1f}s total)"}
+            from monocular_visual_odometry_va4mr_amd.ate import ate
+            rmse, rel = ate(pos_gpu, pos_cpu)
+            out["ate_vs_ref"] = {"rmse": float(rmse), "rel_path": float(rel), "frames": int(len(pos_cpu)),
+                                 "gpu_status": int(st)}
+        else:
+            out["cpu_baseline"] = None
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out))

@@ -366,12 +366,18 @@ VO_DEV CamK camk(const double* K)
 
 VO_DEV void jacobi_eig4(double* S, double* ev, double* U)
 {
+#pragma unroll
     for (int i = 0; i < 16; ++i) U[i] = (i % 5 == 0) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 50; ++sweep) {
         double off = 0;
-        for (int i = 0; i < 4; ++i) for (int j = i + 1; j < 4; ++j) off += S[i * 4 + j] * S[i * 4 + j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i + 1; j < 4; ++j) off += S[i * 4 + j] * S[i * 4 + j];
         if (off < 1e-300) break;
+#pragma unroll
         for (int p = 0; p < 3; ++p) {
+#pragma unroll
             for (int q = p + 1; q < 4; ++q) {
                 double apq = S[p * 4 + q];
                 if (apq == 0.0) continue;
@@ -379,16 +385,19 @@ VO_DEV void jacobi_eig4(double* S, double* ev, double* U)
                 double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
                 if (theta < 0) t = -t;
                 double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     double skp = S[k * 4 + p], skq = S[k * 4 + q];
                     S[k * 4 + p] = c * skp - s * skq;
                     S[k * 4 + q] = s * skp + c * skq;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     double spk = S[p * 4 + k], sqk = S[q * 4 + k];
                     S[p * 4 + k] = c * spk - s * sqk;
                     S[q * 4 + k] = s * spk + c * sqk;
                 }
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     double ukp = U[k * 4 + p], ukq = U[k * 4 + q];
                     U[k * 4 + p] = c * ukp - s * ukq;
@@ -397,6 +406,7 @@ VO_DEV void jacobi_eig4(double* S, double* ev, double* U)
             }
         }
     }
+#pragma unroll
     for (int i = 0; i < 4; ++i) ev[i] = S[i * 4 + i];
 }
 
@@ -422,9 +432,11 @@ VO_DEV void align_horn(const double M[3][3], const double P[3][3], double* R, do
     N[7] = N[13] = s[6] + s[2];
     N[11] = N[14] = s[7] + s[5];
     jacobi_eig4(N, ev, U);
-    int ib = 0;
-    for (int i = 1; i < 4; ++i) if (ev[i] > ev[ib]) ib = i;
-    double q0 = U[0 * 4 + ib], q1 = U[1 * 4 + ib], q2 = U[2 * 4 + ib], q3 = U[3 * 4 + ib];
+    // column of the largest eigenvalue (first on ties), selected with constant indices
+    double q0 = U[0], q1 = U[4], q2 = U[8], q3 = U[12], eb = ev[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (ev[i] > eb) { eb = ev[i]; q0 = U[i]; q1 = U[4 + i]; q2 = U[8 + i]; q3 = U[12 + i]; }
     R[0] = q0 * q0 + q1 * q1 - q2 * q2 - q3 * q3;
     R[1] = 2. * (q1 * q2 - q0 * q3);
     R[2] = 2. * (q1 * q3 + q0 * q2);

@@ -9,6 +9,7 @@
 // integer stages are bit-exact and the float stages use the same op order (built with
 // -ffp-contract=off, correctly rounded f32 div/sqrt).
 #include "vo_dev.h"
+#include <stdlib.h>
 
 #include <float.h>
 
@@ -103,10 +104,10 @@ struct LKParams {
 // (hardware dispatch is round-robin over the 8 XCDs by linear block id), so the chain's
 // pyramid level stays in that XCD's 4 MB L2 instead of being fetched by all eight.
 // The mapping only affects speed; any block order gives the same results.
-VO_DEV bool lk_block(int B, int nb, int& b, int& pb)
+VO_DEV bool lk_block(int B, int nb, int& b, int& pb, bool xcd = true)
 {
     const int L = blockIdx.x;
-    if (B >= 8) {
+    if (B >= 8 && xcd) {
         const int xcd = L & 7, k = L >> 3;
         b = xcd + 8 * (k / nb);
         pb = k % nb;
@@ -350,7 +351,7 @@ __global__ void __launch_bounds__(64) k_lk(LKParams P, int level, int B, int nb)
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
 template <int WW, int WH>
-__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int nb)
+__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int nb, int xcd)
 {
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
     const uint8_t* jr8 = (const uint8_t*)JR;
     const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb;
-    if (!lk_block(B, nb, b, pb)) return;
+    if (!lk_block(B, nb, b, pb, xcd != 0)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
     const int lane = lane_id();
     const int n0 = P.n0 ? P.n0[b] : 0;
@@ -408,13 +409,19 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
     for (int p = pb + 0; p < ntot; p += nb) {
         const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
         const int64_t oidx = (int64_t)b * P.ocap + p;
-        const float ptx = src[0], pty = src[1];
+        // per-point values are wave-uniform: keep them (and the addresses built from them)
+        // in scalar registers
+        const float ptx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(src[0])));
+        const float pty = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(src[1])));
         int status = 1;
         float errv = 0.f;
         float px = ptx * sc, py = pty * sc;
         float ox, oy;   // nextPts[ptidx]
         if (level == P.L) { ox = px; oy = py; }
-        else { ox = P.out[2 * oidx] * 2.f; oy = P.out[2 * oidx + 1] * 2.f; }
+        else {
+            ox = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.out[2 * oidx]))) * 2.f;
+            oy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.out[2 * oidx + 1]))) * 2.f;
+        }
         px -= hx;
         py -= hy;
         const int ipx = (int)floorf(px), ipy = (int)floorf(py);
@@ -424,6 +431,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
                 break;
             }
             // stage I (u8) and dI (int16 x2) rows under the window
+            bool staged = false;
             {
                 const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
                 const int ish = gx & 3;
@@ -476,7 +484,6 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
                 D = 1.f / D;
                 float nx = ox - hx, ny = oy - hy;
                 float pdx = 0.f, pdy = 0.f;
-                bool staged = false;
                 for (int it = 0; it < P.max_count; ++it) {
                     const int inx = (int)floorf(nx), iny = (int)floorf(ny);
                     if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
@@ -1109,7 +1116,9 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     // must free as soon as its own points are done), 1024 blocks per chain: with B >= 8 one
     // XCD (32 CUs) holds about one chain at a time, which keeps that chain's level resident
     // in the XCD's L2.
-    const int nb = 1024;
+    static const int nb_env = [] { const char* e = getenv("VO_LK_NB"); return e ? atoi(e) : 0; }();
+    static const int xcd_env = [] { const char* e = getenv("VO_LK_XCD"); return e ? atoi(e) : 0; }();
+    const int nb = nb_env > 0 ? nb_env : 1024;
     const int nblk = (B >= 8 ? ((B + 7) / 8) * 8 : B) * nb;
     // the LDS-staged 15x15 kernel reads whole dwords: it needs >= 64 bytes of slack after
     // the last pyramid level
@@ -1119,7 +1128,7 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     const size_t lds = 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
     if (lds > 60 * 1024) return VO_EARG;
     for (int level = P.L; level >= 0; --level) {
-        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, B, nb);
+        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, B, nb, xcd_env);
         else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
         else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }

@@ -12,6 +12,13 @@ namespace {
 
 using namespace vg;
 
+#ifdef VO_PNP_PROF
+__device__ long long g_pnpprof[32];
+#define PNPPROF(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pnpprof[i] = wall_clock64(); } while (0)
+#else
+#define PNPPROF(i) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------ EPnP (block)
 struct EpnpShared {
     double cws[4][3], ccs[4][3];
@@ -308,6 +315,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         a[0] = 1.0 - a[1] - a[2] - a[3];
     }
     __syncthreads();
+    PNPPROF(10);
     // M^T M upper triangle (78 entries): one pass over the points, 4 waves x ~20 entries
     const double fu = K[0], fv = K[4], uc = K[2], vc = K[5];
     __shared__ double up[78];
@@ -329,6 +337,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         svd_jacobi_wave<12, 12>(S.MtM, S.dM, S.V12);
     }
     __syncthreads();
+    PNPPROF(11);
     if (tid == 0) {
         epnp_L6x10(S.V12, S.L);
         for (int j = 0; j < 6; ++j) {
@@ -336,6 +345,10 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
             const double* r = S.cws[PAIR_B[j]];
             S.rho[j] = (p[0] - r[0]) * (p[0] - r[0]) + (p[1] - r[1]) * (p[1] - r[1]) + (p[2] - r[2]) * (p[2] - r[2]);
         }
+    }
+    __syncthreads();
+    // the three beta approximations are independent: one thread each, on different waves
+    if (tid == 0) {
         {
             double A[24], b4[4];
             const int cols[4] = {0, 1, 3, 6};
@@ -346,6 +359,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
             else { B[0] = sqrt(b4[0]); B[1] = b4[1] / B[0]; B[2] = b4[2] / B[0]; B[3] = b4[3] / B[0]; }
             epnp_gauss_newton(S.L, S.rho, B);
         }
+    } else if (tid == 64) {
         {
             double A[18], b3[3];
             for (int i = 0; i < 6; ++i) for (int j = 0; j < 3; ++j) A[i * 3 + j] = S.L[i * 10 + j];
@@ -357,6 +371,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
             B[2] = 0.0; B[3] = 0.0;
             epnp_gauss_newton(S.L, S.rho, B);
         }
+    } else if (tid == 128) {
         {
             double A[30], b5[5];
             for (int i = 0; i < 6; ++i) for (int j = 0; j < 5; ++j) A[i * 5 + j] = S.L[i * 10 + j];
@@ -370,9 +385,11 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         }
     }
     __syncthreads();
+    PNPPROF(12);
     // the oracle runs approximation 1's R,t before computing approximation 2's betas; the
     // betas do not depend on R,t, so computing all betas first is equivalent
     for (int a = 1; a <= 3; ++a) epnp_R_and_t(S, a, K, pws, us, alphas, pcs, n);
+    PNPPROF(13);
     if (tid == 0) {
         int N = 1;
         if (S.rep[2] < S.rep[1]) N = 2;
@@ -446,6 +463,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         }
         return;
     }
+    PNPPROF(0);
     uint64_t rng = ~0ULL;   // only thread 0's copy is used
     if (tid == 0) { sh[0] = 0; sh[1] = A.iters > 1 ? A.iters : 1; sh[2] = 0; }
     __syncthreads();
@@ -453,6 +471,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         const int it0 = sh[0];
         const int niters0 = sh[1];
         if (it0 >= niters0) break;
+        PNPPROF(1);
         if (tid == 0) {
             for (int h = 0; h < HYP; ++h) {
                 for (int i = 0; i < 4; ++i) {
@@ -483,6 +502,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
             }
         }
         __syncthreads();
+        PNPPROF(2);
         {
             const int w = wave_id(), lane = lane_id();
             const int hpw = HYP / (blockDim.x >> 6);
@@ -516,6 +536,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         }
         __syncthreads();
     }
+    PNPPROF(3);
     if (sh[2] <= 0) {
         if (tid == 0) { A.success[b] = 0; A.n_inl[b] = 0; }
         for (int i = tid; i < n; i += blockDim.x) mask[i] = 0;
@@ -547,7 +568,9 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
     }
     __syncthreads();
     __shared__ double Rfin[9], tfin[3];
+    PNPPROF(4);
     epnp_block(S, A.K, pws, us, alphas, pcs, m, Rfin, tfin);
+    PNPPROF(5);
     if (tid == 0) {
         rodrigues_m2v(Rfin, A.rvec + 3 * b);
         for (int q = 0; q < 3; ++q) A.tvec[3 * b + q] = tfin[q];

@@ -232,6 +232,14 @@ class Engine:
         g.replay()
         self.prev = 1 - self.prev
 
+    def step_graph(self, frames):
+        """Same as step(), replayed from a captured hipGraph (one launch per frame; the
+        frames are copied into the graph's bound input buffer first)."""
+        if not self._graphs:
+            self.capture_step()
+        self._graphs["buf"].copy_(self._frames(frames))
+        self.replay_step()
+
     # ------------------------------------------------------------------ bootstrap
     def bootstrap(self, img0, img1):
         """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:

@@ -5,7 +5,8 @@ from separate --pmc FETCH_SIZE / WRITE_SIZE passes, per-launch HBM bytes.
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE (KB) counts half the bytes of
 wide coalesced reads -> x2; WRITE_SIZE (KB) is taken as is.
 
-usage: prof_summary.py <tag> <prof_dir> [fetch_dir write_dir] [--chains B] [--steps N]
+usage: prof_summary.py <tag> <prof_dir> [fetch_dir write_dir] [--chains B] [--steps N] [--groups G]
+(--chains = chains per engine group, i.e. per launch)
 (--steps N = warmup + timed steps of the profiled bench run: per-stage bytes are per step,
 i.e. each kernel's mean bytes x its launches per step)
 writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_summary.md and (with PMC dirs)
@@ -51,11 +52,14 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     chains = None
     nsteps = None
+    groups = 1
+    if "--groups" in sys.argv:
+        groups = int(sys.argv[sys.argv.index("--groups") + 1])
     if "--chains" in sys.argv:
         chains = int(sys.argv[sys.argv.index("--chains") + 1])
     if "--steps" in sys.argv:
         nsteps = int(sys.argv[sys.argv.index("--steps") + 1])
-    flag_vals = {sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a in ("--chains", "--steps")}
+    flag_vals = {sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a in ("--chains", "--steps", "--groups")}
     args = [a for a in args if a not in flag_vals]
     tag, prof = args[0], args[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -82,8 +86,9 @@ def main():
         lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['TotalDurationNs']) / 1e6:.2f} | {fs} | {ws} |")
         if fb is not None and wb is not None and k in STAGE_OF:
             st = STAGE_OF[k]
-            e = traffic.setdefault(st, {"bytes_per_launch": 0.0, "kernels": {}, "chains": chains, "tag": tag})
-            per_step = max(1, round(int(r["Calls"]) / nsteps)) if nsteps else 1
+            e = traffic.setdefault(st, {"bytes_per_launch": 0.0, "kernels": {}, "chains": chains,
+                                        "groups": groups, "tag": tag})
+            per_step = max(1, round(int(r["Calls"]) / (nsteps * groups))) if nsteps else 1
             b = (2 * fb * 1024 + wb * 1024) * per_step
             e["kernels"][k] = {"bytes_per_step": b, "launches_per_step": per_step}
             e["bytes_per_launch"] += b
