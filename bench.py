@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-single", action="store_true", help="skip the single-chain latency / CPU leg "
+                    "(profiling runs of the batched workload)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (see profiles/)")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
@@ -327,7 +329,7 @@ def main():
         "gather_ms": round(gather_ms, 3),
     }
 
-    if world == 1 and args.cpu_frames > 2:
+    if world == 1 and args.cpu_frames > 2 and not args.no_single:
         sample = render_windows(rend, gt, [0], gap, args.cpu_frames - 2, device)[:, 0]
         pos_gpu, st, lat, lat_g, same = gpu_chain_positions(Kmat, opts, sample, device)
         out["single_chain"] = {"frames_per_s": round(1.0 / lat, 1), "ms_per_frame": round(lat * 1e3, 3),

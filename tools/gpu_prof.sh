@@ -5,9 +5,9 @@ tag=$1; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R="--output-format csv"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats $R -d gpurun_out/prof_$tag -o run -- python bench.py --no-cpu "$@" > gpurun_out/prof_$tag.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats $R -d gpurun_out/prof_$tag -o run -- python bench.py --no-cpu --no-single "$@" > gpurun_out/prof_$tag.log 2>&1 || exit $?
 ls -la gpurun_out/prof_$tag/*
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "::k_" $R -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py --no-cpu "$@" > gpurun_out/pmc_fetch_$tag.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "::k_" $R -d gpurun_out/pmc_write_$tag -o run -- python bench.py --no-cpu "$@" > gpurun_out/pmc_write_$tag.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "::k_" $R -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py --no-cpu --no-single "$@" > gpurun_out/pmc_fetch_$tag.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "::k_" $R -d gpurun_out/pmc_write_$tag -o run -- python bench.py --no-cpu --no-single "$@" > gpurun_out/pmc_write_$tag.log 2>&1 || exit $?
 du -sh gpurun_out/*
 rm -f gpurun_out/prof_$tag/*kernel_trace.csv

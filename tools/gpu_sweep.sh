@@ -4,6 +4,6 @@ tag=$1; shift
 mkdir -p gpurun_out
 for bg in $1; do
   b=${bg%:*}; g=${bg#*:}
-  timeout -k 10 300 python bench.py --no-cpu --chains $b --groups $g --steps 20 > gpurun_out/sweep_${tag}_${b}_${g}.json 2>gpurun_out/sweep_${tag}_${b}_${g}.err || exit $?
+  timeout -k 10 300 python bench.py --no-cpu --no-single --chains $b --groups $g --steps 20 > gpurun_out/sweep_${tag}_${b}_${g}.json 2>gpurun_out/sweep_${tag}_${b}_${g}.err || exit $?
   python -c "import json,sys; d=json.load(open('gpurun_out/sweep_${tag}_${b}_${g}.json')); print('B=$b G=$g', d['value'], d['ms_per_step'], d.get('host_ms_per_step'), d['stages_ms'], d['chain_status'])"
 done
