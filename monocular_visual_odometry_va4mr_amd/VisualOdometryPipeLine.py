@@ -12,7 +12,9 @@ Same constructor, methods and public attributes as
     .outlier_pts_current, .num_tracked_landmarks_list, .potential_frame, .K, .K_inv
 
 The whole hot path runs on the GPU through libvo_hip.so (engine.Engine with one chain);
-state stays in HBM and the attributes are read back on access.  The reference's failure
+state stays in HBM and the attributes are read back on access.  The per-frame step is
+captured once into a pair of hipGraphs (ping-pong pyramids) and replayed for every frame
+(SURVEY.md §8f item 1); ``use_graph=False`` launches the stages one by one instead.  The reference's failure
 conditions raise the same exceptions: ValueError("Not enough keypoints for PnP") (:358),
 ValueError("PnP failed") (:352), and the crashes the reference would hit when
 goodFeaturesToTrack yields 0 / 1 corners (:256-258).
@@ -27,7 +29,7 @@ from .engine import Engine
 
 class VisualOdometryPipeLine:
     def __init__(self, K, options, max_frames: int = 8192, landmark_capacity: int = 16384,
-                 candidate_capacity: int = 16384, device=None):
+                 candidate_capacity: int = 16384, device=None, use_graph: bool = True):
         self.options = options
         self.K = K
         self.K_inv = np.linalg.inv(K)
@@ -35,6 +37,7 @@ class VisualOdometryPipeLine:
         self.num_tracked_landmarks_list = []
         self._caps = (int(landmark_capacity), int(candidate_capacity), int(max_frames))
         self._device = device
+        self._use_graph = bool(use_graph)     # per-frame step replayed from a captured hipGraph
         self._eng: Engine | None = None
         self._frame = None
         self._boot_done = False
@@ -75,7 +78,10 @@ class VisualOdometryPipeLine:
         if not self._boot_done:
             raise RuntimeError("initialization() must run first")
         eng = self._eng
-        eng.step(np.asarray(img)[None])
+        if self._use_graph:
+            eng.step_graph(np.asarray(img)[None])
+        else:
+            eng.step(np.asarray(img)[None])
         self._frame = np.asarray(img)
         st = self._status()
         if st == L.ST_OK:

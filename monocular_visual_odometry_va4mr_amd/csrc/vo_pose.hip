@@ -471,9 +471,12 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         const int it0 = sh[0];
         const int niters0 = sh[1];
         if (it0 >= niters0) break;
+        // a small first round: with the usual inlier ratios the adaptive iteration count
+        // drops below 16 there, and fewer diverging P3P lanes finish sooner
+        const int CH = it0 == 0 ? HYP / 4 : HYP;
         PNPPROF(1);
         if (tid == 0) {
-            for (int h = 0; h < HYP; ++h) {
+            for (int h = 0; h < CH; ++h) {
                 for (int i = 0; i < 4; ++i) {
                     for (;;) {
                         int v = (int)(rng_next(rng) % (uint32_t)n);
@@ -486,7 +489,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
             }
         }
         __syncthreads();
-        if (tid < HYP) {
+        if (tid < CH) {
             const int h = tid;
             double o[12], im[8], R[9], t[3];
             for (int j = 0; j < 4; ++j) {
@@ -505,7 +508,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         PNPPROF(2);
         {
             const int w = wave_id(), lane = lane_id();
-            const int hpw = HYP / (blockDim.x >> 6);
+            const int hpw = CH / (blockDim.x >> 6);
             for (int h = w * hpw; h < (w + 1) * hpw; ++h) {
                 if (!valid[h]) { if (lane == 0) cnt[h] = 0; continue; }
                 const double* R = mdl[h];
@@ -520,7 +523,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         __syncthreads();
         if (tid == 0) {
             int niters = sh[1], best = sh[2];
-            for (int h = 0; h < HYP; ++h) {
+            for (int h = 0; h < CH; ++h) {
                 if (it0 + h >= niters) break;
                 if (!valid[h]) continue;
                 const int good = cnt[h];
@@ -530,7 +533,7 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
                     niters = ransac_update_niters(A.conf, (double)(n - good) / n, 4, niters);
                 }
             }
-            sh[0] = it0 + HYP;
+            sh[0] = it0 + CH;
             sh[1] = niters;
             sh[2] = best;
         }
