@@ -174,6 +174,97 @@ VO_DEV void svd_jacobi_wave(double* A, double* w, double* V)
     wave_lds_sync();
 }
 
+// Round-robin Jacobi SVD (oracle/vo_oracle_geom.c svd_jacobi_rr) by one wave, A [M*N], w [N],
+// V [N*N] and cs [N/2 * 3] in LDS, N even.  Round r pairs the columns by the circle method; the
+// N/2 pairs of a round are disjoint, so lane p < N/2 forms pair p's sums (scalar order) and
+// rotation, and then every lane applies all of the round's rotations to its row.
+template <int M, int N>
+VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
+{
+    static_assert(N % 2 == 0 && N <= 64 && M <= 64, "round-robin SVD needs even N <= 64");
+    constexpr int NP = N / 2;
+    const int lane = lane_id();
+    for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
+    wave_lds_sync();
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        bool changed = false;
+        for (int r = 0; r < N - 1; ++r) {
+            if (lane < NP) {
+                const int q = lane;
+                const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
+                const int b = ((N - 2 - q + r) % (N - 1)) + 1;
+                const int i = a < b ? a : b, j = a < b ? b : a;
+                double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    double ai = A[k * N + i], aj = A[k * N + j];
+                    alpha += ai * ai;
+                    beta += aj * aj;
+                    gamma += ai * aj;
+                }
+                double c = 1.0, s = 0.0, f = 0.0;
+                if (alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta))) {
+                    double zeta = (beta - alpha) / (2.0 * gamma);
+                    double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    if (zeta < 0) t = -t;
+                    c = 1.0 / sqrt(1.0 + t * t);
+                    s = c * t;
+                    f = 1.0;
+                }
+                cs[3 * q] = c;
+                cs[3 * q + 1] = s;
+                cs[3 * q + 2] = f;
+            }
+            wave_lds_sync();
+            for (int q = 0; q < NP; ++q) {
+                if (cs[3 * q + 2] == 0.0) continue;
+                changed = true;
+                const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
+                const int b = ((N - 2 - q + r) % (N - 1)) + 1;
+                const int i = a < b ? a : b, j = a < b ? b : a;
+                const double c = cs[3 * q], s = cs[3 * q + 1];
+                if (lane < M) {
+                    double ai = A[lane * N + i], aj = A[lane * N + j];
+                    A[lane * N + i] = c * ai - s * aj;
+                    A[lane * N + j] = s * ai + c * aj;
+                }
+                if (lane < N) {
+                    double vi = V[lane * N + i], vj = V[lane * N + j];
+                    V[lane * N + i] = c * vi - s * vj;
+                    V[lane * N + j] = s * vi + c * vj;
+                }
+            }
+            wave_lds_sync();
+        }
+        if (!changed) break;
+    }
+    for (int i = 0; i < N; ++i) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) s += A[k * N + i] * A[k * N + i];
+        if (lane == 0) w[i] = sqrt(s);
+    }
+    wave_lds_sync();
+    for (int i = 0; i < N - 1; ++i) {
+        int b = i;
+        for (int j = i + 1; j < N; ++j) if (w[j] > w[b]) b = j;
+        if (b != i) {
+            wave_lds_sync();
+            if (lane == 0) { double tw = w[i]; w[i] = w[b]; w[b] = tw; }
+            if (lane < M) { double t = A[lane * N + i]; A[lane * N + i] = A[lane * N + b]; A[lane * N + b] = t; }
+            if (lane < N) { double t = V[lane * N + i]; V[lane * N + i] = V[lane * N + b]; V[lane * N + b] = t; }
+            wave_lds_sync();
+        }
+    }
+    for (int i = 0; i < N; ++i) {
+        if (w[i] > 0) {
+            double inv = 1.0 / w[i];
+            if (lane < M) A[lane * N + i] *= inv;
+        }
+    }
+    wave_lds_sync();
+}
+
 template <int M, int N>
 VO_DEV void lsq_svd(const double* A_in, const double* b, double* x)
 {

@@ -326,7 +326,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         default: epnp_mtm_part<60, 78>(n, alphas, us, fu, fv, uc, vc, up); break;
     }
     __syncthreads();
-    // 12x12 Jacobi SVD of M^T M by wave 0 in LDS
+    // 12x12 round-robin Jacobi SVD of M^T M by wave 0 in LDS (oracle: svd_jacobi_rr)
     if (wave_id() == 0) {
         for (int q = lane_id(); q < 144; q += 64) {
             int a = q / 12, bb = q - a * 12;
@@ -334,7 +334,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
             S.MtM[q] = up[a * 12 - a * (a - 1) / 2 + (bb - a)];
         }
         wave_lds_sync();
-        svd_jacobi_wave<12, 12>(S.MtM, S.dM, S.V12);
+        svd_jacobi_wave_rr<12, 12>(S.MtM, S.dM, S.V12, S.tmp);
     }
     __syncthreads();
     PNPPROF(11);

@@ -96,6 +96,75 @@ static void svd_jacobi(double* A, int m, int n, double* w, double* V)
     }
 }
 
+/* Round-robin ("parallel ordering") one-sided Jacobi SVD for even n.  Each sweep runs n-1
+ * rounds; round r pairs the columns by the circle method (column 0 fixed, the others
+ * rotated by r), so a round's rotations touch disjoint column pairs and may be applied in any
+ * order (or all at once, as the GPU does).  Same per-rotation arithmetic, stopping rule,
+ * sort and normalisation as svd_jacobi; used for EPnP's 12x12 M^T M.  (OpenCV's JacobiSVD
+ * uses the cyclic order; the decompositions agree to rounding -- OpenCV-level parity is
+ * unpinned anyway, and the GPU follows this order exactly.) */
+static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
+{
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        int changed = 0;
+        for (int r = 0; r < n - 1; ++r) {
+            for (int q = 0; q < n / 2; ++q) {
+                const int a = q == 0 ? 0 : ((q - 1 + r) % (n - 1)) + 1;
+                const int b = ((n - 2 - q + r) % (n - 1)) + 1;
+                const int i = a < b ? a : b, j = a < b ? b : a;
+                double alpha = 0, beta = 0, gamma = 0;
+                for (int k = 0; k < m; ++k) {
+                    double ai = A[k * n + i], aj = A[k * n + j];
+                    alpha += ai * ai;
+                    beta += aj * aj;
+                    gamma += ai * aj;
+                }
+                if (alpha == 0.0 || beta == 0.0) continue;
+                if (fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
+                changed = 1;
+                double zeta = (beta - alpha) / (2.0 * gamma);
+                double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                if (zeta < 0) t = -t;
+                double c = 1.0 / sqrt(1.0 + t * t);
+                double s = c * t;
+                for (int k = 0; k < m; ++k) {
+                    double ai = A[k * n + i], aj = A[k * n + j];
+                    A[k * n + i] = c * ai - s * aj;
+                    A[k * n + j] = s * ai + c * aj;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double vi = V[k * n + i], vj = V[k * n + j];
+                    V[k * n + i] = c * vi - s * vj;
+                    V[k * n + j] = s * vi + c * vj;
+                }
+            }
+        }
+        if (!changed) break;
+    }
+    for (int i = 0; i < n; ++i) {
+        double s = 0;
+        for (int k = 0; k < m; ++k) s += A[k * n + i] * A[k * n + i];
+        w[i] = sqrt(s);
+    }
+    for (int i = 0; i < n - 1; ++i) {
+        int b = i;
+        for (int j = i + 1; j < n; ++j) if (w[j] > w[b]) b = j;
+        if (b != i) {
+            double tw = w[i]; w[i] = w[b]; w[b] = tw;
+            for (int k = 0; k < m; ++k) { double t = A[k * n + i]; A[k * n + i] = A[k * n + b]; A[k * n + b] = t; }
+            for (int k = 0; k < n; ++k) { double t = V[k * n + i]; V[k * n + i] = V[k * n + b]; V[k * n + b] = t; }
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        if (w[i] > 0) {
+            double inv = 1.0 / w[i];
+            for (int k = 0; k < m; ++k) A[k * n + i] *= inv;
+        }
+    }
+}
+
 /* least squares min ||A x - b|| via SVD pseudo-inverse (cv::solve DECOMP_SVD) */
 static void lsq_svd(const double* A_in, int m, int n, const double* b, double* x)
 {
@@ -775,7 +844,7 @@ int vo_o_epnp(const double* K, const double* obj, const double* img, int n, doub
     det_sum(&e, c_mtm, n, 78, up);
     int q = 0;
     for (int a = 0; a < 12; ++a) for (int b = a; b < 12; ++b) { MtM[a * 12 + b] = MtM[b * 12 + a] = up[q++]; }
-    svd_jacobi(MtM, 12, 12, dM, V12);
+    svd_jacobi_rr(MtM, 12, 12, dM, V12);
     double L[60], rho[6];
     epnp_L6x10(V12, L);
     for (int j = 0; j < 6; ++j) {

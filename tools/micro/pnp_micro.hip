@@ -13,7 +13,7 @@ __global__ void k_t_svd(const double* Min, double* out, long long* t)
     for (int i = threadIdx.x; i < 144; i += 64) A[i] = Min[i];
     __syncthreads();
     long long c0 = clock64();
-    vg::svd_jacobi_wave<12, 12>(A, w, V);
+    { __shared__ double cs[18]; vg::svd_jacobi_wave_rr<12, 12>(A, w, V, cs); }
     long long c1 = clock64();
     if (threadIdx.x == 0) {
         t[0] = c1 - c0;
