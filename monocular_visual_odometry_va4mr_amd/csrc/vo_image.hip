@@ -16,61 +16,113 @@
 namespace {
 
 // ------------------------------------------------------------------ pyramid
-__global__ void k_ingest(const uint8_t* __restrict__ frames, int64_t fstride, uint8_t* __restrict__ pyr,
-                         int64_t pstride, int W, int H, int pitch, int64_t off)
+// Levels are stored with a materialised VO_BORDER reflect-101 border and a 64-byte-multiple
+// pitch.  One wave per row (256-thread blocks cover 4 rows); every lane writes an aligned
+// vector (16, 4 or 16 bytes).  Bytes between the padded width and the pitch may be written
+// with don't-care values.
+
+// level 0 (frame copy + border): a wave writes 1024 output bytes of one row, 16 per lane; the
+// (unaligned) source row segment is first read into LDS with coalesced loads
+__global__ void __launch_bounds__(256) k_ingest(const uint8_t* __restrict__ frames, int64_t fstride,
+                                                uint8_t* __restrict__ pyr, int64_t pstride, int W, int H,
+                                                int pitch, int64_t off, int ph)
 {
+    __shared__ uint8_t segs[4][1024 + 4];
+    uint8_t* seg = segs[wave_id()];
     const int b = blockIdx.z;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x;
-    const int py = blockIdx.y;
-    if (px >= W + 2 * VO_BORDER) return;
-    const int sx = refl101(px - VO_BORDER, W), sy = refl101(py - VO_BORDER, H);
-    pyr[b * pstride + off + (int64_t)py * pitch + px] = frames[b * fstride + (int64_t)sy * W + sx];
+    const int x0 = blockIdx.x * 1024;                 // first output column of this wave
+    const int py = blockIdx.y * 4 + wave_id();
+    const int pw = W + 2 * VO_BORDER;
+    if (py >= ph) return;
+    const uint8_t* srow = frames + b * fstride + (int64_t)refl101(py - VO_BORDER, H) * W;
+    // interior source columns covered here: [x0 - B, x0 + 1024 - B) clipped to [0, W)
+    const int s0 = max(x0 - VO_BORDER, 0), s1 = min(x0 + 1024 - VO_BORDER, W);
+    const int lane = lane_id();
+    for (int i = lane; i < s1 - s0; i += 64) seg[i] = srow[s0 + i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int px0 = x0 + lane * 16;
+    if (px0 >= pw) return;
+    uint32_t w4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int px = px0 + 4 * q + k;
+            uint32_t byte = 0;
+            if (px < pw) {
+                const int sx = refl101(px - VO_BORDER, W);
+                byte = (sx >= s0 && sx < s1) ? seg[sx - s0] : srow[sx];   // borders: reflected
+            }
+            v |= byte << (8 * k);
+        }
+        w4[q] = v;
+    }
+    *(uint4*)(pyr + b * pstride + off + (int64_t)py * pitch + px0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
 }
 
-__global__ void k_pyrdown(uint8_t* __restrict__ pyr, int64_t pstride, int sw, int spitch, int64_t soff,
-                          int dw, int dh, int dpitch, int64_t doff)
+// pyrDown (5x5 [1 4 6 4 1]^2 / 256, cv::pyrDown) into the next level incl. border: 4 pixels
+// per lane; source reads stay inside the source's reflect-101 border (|offset| <= 2)
+__global__ void __launch_bounds__(256) k_pyrdown(uint8_t* __restrict__ pyr, int64_t pstride, int sw, int spitch,
+                                                 int64_t soff, int dw, int dh, int dpitch, int64_t doff)
 {
     const int b = blockIdx.z;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x;
-    const int py = blockIdx.y;
-    if (px >= dw + 2 * VO_BORDER) return;
-    const int ix = refl101(px - VO_BORDER, dw), iy = refl101(py - VO_BORDER, dh);
-    const uint8_t* src = pyr + b * pstride + soff;
-    // source reads stay inside the source's reflect-101 border (|offset| <= 2 < VO_BORDER)
-    const int k5[5] = {1, 4, 6, 4, 1};
-    int acc = 0;
+    const int px0 = (blockIdx.x * 64 + lane_id()) * 4;
+    const int py = blockIdx.y * 4 + wave_id();
+    const int pw = dw + 2 * VO_BORDER;
+    if (px0 >= pw || py >= dh + 2 * VO_BORDER) return;
+    const int iy = refl101(py - VO_BORDER, dh);
+    const uint8_t* src = pyr + b * pstride + soff + (int64_t)(2 * iy - 2 + VO_BORDER) * spitch + VO_BORDER - 2;
+    uint32_t v = 0;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint8_t* row = src + (int64_t)(2 * iy - 2 + i + VO_BORDER) * spitch + (2 * ix - 2 + VO_BORDER);
-        int r = row[0] + 4 * row[1] + 6 * row[2] + 4 * row[3] + row[4];
-        acc += k5[i] * r;
+    for (int k = 0; k < 4; ++k) {
+        const int px = px0 + k;
+        const int ix = refl101(min(px, pw - 1) - VO_BORDER, dw);
+        const uint8_t* col = src + 2 * ix;
+        int acc = 0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint8_t* row = col + (int64_t)i * spitch;
+            const int r = row[0] + 4 * row[1] + 6 * row[2] + 4 * row[3] + row[4];
+            acc += (i == 0 || i == 4 ? 1 : (i == 2 ? 6 : 4)) * r;
+        }
+        v |= (uint32_t)((acc + 128) >> 8) << (8 * k);
     }
     (void)sw;
-    pyr[b * pstride + doff + (int64_t)py * dpitch + px] = (uint8_t)((acc + 128) >> 8);
+    *(uint32_t*)(pyr + b * pstride + doff + (int64_t)py * dpitch + px0) = v;
 }
 
-__global__ void k_scharr(const uint8_t* __restrict__ pyr, int64_t pstride, int16_t* __restrict__ der,
-                         int64_t dstride, int w, int h, int pitch, int64_t off)
+// Scharr (calcSharrDeriv) of one level: int16 (dx, dy) per pixel, zero outside the image
+// (the derivative image's constant border); 4 pixels (16 bytes) per lane
+__global__ void __launch_bounds__(256) k_scharr(const uint8_t* __restrict__ pyr, int64_t pstride,
+                                                int16_t* __restrict__ der, int64_t dstride, int w, int h,
+                                                int pitch, int64_t off)
 {
     const int b = blockIdx.z;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x;
-    const int py = blockIdx.y;
-    if (px >= w + 2 * VO_BORDER) return;
-    int16_t* d = der + b * dstride + 2 * (off + (int64_t)py * pitch + px);
-    const int x = px - VO_BORDER, y = py - VO_BORDER;
-    if (x < 0 || x >= w || y < 0 || y >= h) {
-        d[0] = 0;
-        d[1] = 0;
-        return;
-    }
-    const uint8_t* c = pyr + b * pstride + off + (int64_t)py * pitch + px;
+    const int px0 = (blockIdx.x * 64 + lane_id()) * 4;
+    const int py = blockIdx.y * 4 + wave_id();
+    if (px0 >= w + 2 * VO_BORDER || py >= h + 2 * VO_BORDER) return;
+    const int y = py - VO_BORDER;
+    const uint8_t* c = pyr + b * pstride + off + (int64_t)py * pitch;
     const uint8_t* u = c - pitch;   // reflect-101 border rows/cols are materialised
     const uint8_t* l = c + pitch;
-    int t0l = (u[-1] + l[-1]) * 3 + c[-1] * 10;
-    int t0r = (u[1] + l[1]) * 3 + c[1] * 10;
-    int t1l = l[-1] - u[-1], t1c = l[0] - u[0], t1r = l[1] - u[1];
-    d[0] = (int16_t)(t0r - t0l);
-    d[1] = (int16_t)((t1r + t1l) * 3 + t1c * 10);
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int px = px0 + k, x = px - VO_BORDER;
+        int dx = 0, dy = 0;
+        if (x >= 0 && x < w && y >= 0 && y < h) {
+            const int t0l = (u[px - 1] + l[px - 1]) * 3 + c[px - 1] * 10;
+            const int t0r = (u[px + 1] + l[px + 1]) * 3 + c[px + 1] * 10;
+            const int t1l = l[px - 1] - u[px - 1], t1c = l[px] - u[px], t1r = l[px + 1] - u[px + 1];
+            dx = t0r - t0l;
+            dy = (t1r + t1l) * 3 + t1c * 10;
+        }
+        o[k] = (uint32_t)(uint16_t)(int16_t)dx | ((uint32_t)(uint16_t)(int16_t)dy << 16);
+    }
+    *(uint4*)(der + b * dstride + 2 * (off + (int64_t)py * pitch + px0)) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // ------------------------------------------------------------------ LK
@@ -789,6 +841,8 @@ struct SelParams {
     int32_t* ncorners;
     int mcap;
     uint32_t* gscratch;      // per-chain L2 grid when the LDS grid is too small ([B][W*H] u32)
+    int acc_lds;             // accepted-corner slots in LDS (min(mcap, ACC_MAX))
+    int grid_lds;            // grid cells held in LDS (0: grid in L2)
     int64_t gstride;
     int32_t* chain_status;
 };
@@ -814,9 +868,11 @@ __device__ long long g_selprof[16];
 
 __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
 {
-    __shared__ uint64_t page[PAGE];
-    __shared__ uint32_t lgrid[GRID_LDS_CELLS];
-    __shared__ uint32_t acc_xy[ACC_MAX];
+    // dynamic LDS sized by the host (vo_gftt): page | accepted xy | grid (if it fits)
+    extern __shared__ uint64_t sel_dyn[];
+    uint64_t* page = sel_dyn;
+    uint32_t* acc_xy = (uint32_t*)(sel_dyn + PAGE);
+    uint32_t* lgrid = acc_xy + P.acc_lds;
     __shared__ uint32_t round_xy[64];
     __shared__ int hist[256];
     __shared__ int sh_int[16];
@@ -854,9 +910,9 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
     const int gw = (P.W + cs - 1) / cs, gh = (P.H + cs - 1) / cs;
     const double md2 = md * md;
     const int want = P.max_corners > 0 ? P.max_corners : 0x7FFFFFFF;
-    const int cap = P.mcap < ACC_MAX ? P.mcap : ACC_MAX;
+    const int cap = P.mcap < P.acc_lds ? P.mcap : P.acc_lds;
     const int limit = want < cap ? want : cap;
-    const bool lds = (int64_t)gw * gh <= GRID_LDS_CELLS;
+    const bool lds = (int64_t)gw * gh <= P.grid_lds;
     uint32_t* gg = P.gscratch + (int64_t)b * P.gstride;
     if (use_grid) {
         for (int q = tid; q < gw * gh; q += blockDim.x) cell_set(lds, lgrid, gg, q, 0xFFFFFFFFu);
@@ -1055,13 +1111,13 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
     uint8_t* pyr = s->pyr[cur];
     {
         const int pw = d->W + 2 * VO_BORDER, ph = d->H + 2 * VO_BORDER;
-        dim3 g((pw + 255) / 256, ph, d->B);
+        dim3 g((pw + 1023) / 1024, (ph + 3) / 4, d->B);
         hipLaunchKernelGGL(k_ingest, g, dim3(256), 0, VO_STREAM(stream), frames, frame_stride, pyr, d->pyr_stride,
-                           d->W, d->H, d->lvl_pitch[0], d->lvl_off[0]);
+                           d->W, d->H, d->lvl_pitch[0], d->lvl_off[0], ph);
     }
     for (int l = 1; l < d->nlev; ++l) {
         const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
-        dim3 g((pw + 255) / 256, ph, d->B);
+        dim3 g((pw + 4 * 64 - 1) / (4 * 64), (ph + 3) / 4, d->B);
         hipLaunchKernelGGL(k_pyrdown, g, dim3(256), 0, VO_STREAM(stream), pyr, d->pyr_stride, d->lvl_w[l - 1],
                            d->lvl_pitch[l - 1], d->lvl_off[l - 1], d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l],
                            d->lvl_off[l]);
@@ -1074,7 +1130,7 @@ extern "C" int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_s
     if (!d || !s || which < 0 || which > 1) return VO_EARG;
     for (int l = 0; l < d->nlev; ++l) {
         const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
-        dim3 g((pw + 255) / 256, ph, d->B);
+        dim3 g((pw + 4 * 64 - 1) / (4 * 64), (ph + 3) / 4, d->B);
         hipLaunchKernelGGL(k_scharr, g, dim3(256), 0, VO_STREAM(stream), s->pyr[which], d->pyr_stride, s->der,
                            d->der_stride, d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l], d->lvl_off[l]);
     }
@@ -1207,6 +1263,19 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
     S.corners = s->corners; S.ncorners = s->nCorners; S.mcap = d->mcap; S.chain_status = s->status;
     S.gscratch = (uint32_t*)s->eig;      // L2 grid when the LDS grid is too small
     S.gstride = (int64_t)d->W * d->H;
-    hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), 0, st, S);
+    {
+        // LDS sized to this configuration (page + corner cap + grid) instead of the maximum
+        const double md = o->feature_min_dist;
+        const int cs = md >= 1 ? (int)lrint(md) : 1;
+        const int64_t cells = md >= 1 ? (int64_t)((d->W + cs - 1) / cs) * ((d->H + cs - 1) / cs) : 0;
+        S.acc_lds = d->mcap < ACC_MAX ? d->mcap : ACC_MAX;
+        S.grid_lds = cells <= GRID_LDS_CELLS ? (int)cells : 0;
+        const size_t lds = 8 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 4 * (size_t)S.grid_lds;
+        static const bool attr_ok = hipFuncSetAttribute((const void*)k_gftt_select,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        8 * PAGE + 4 * ACC_MAX + 4 * GRID_LDS_CELLS) == hipSuccess;
+        if (!attr_ok && lds > 64 * 1024) return VO_EHIP;
+        hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), lds, st, S);
+    }
     return hip_ok() ? VO_OK : VO_EHIP;
 }

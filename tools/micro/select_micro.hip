@@ -27,6 +27,8 @@ int main()
     S.keys = dk; S.nkeys = dn; S.eig_max = dmax; S.quality = 0.1; S.ccap = ccap; S.W = W; S.H = H;
     S.max_corners = 1400; S.min_dist = 10; S.corners = dcor; S.ncorners = dnc; S.mcap = mcap;
     S.gscratch = dgrid; S.gstride = (int64_t)W * H; S.chain_status = dst;
+    S.acc_lds = mcap; S.grid_lds = ((W + 9) / 10) * ((H + 9) / 10);
+    const size_t lds = 8 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 4 * (size_t)S.grid_lds;
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int rep = 0; rep < 4; ++rep) {
         CK(hipMemcpy(dk, keys.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
@@ -34,7 +36,7 @@ int main()
         CK(hipMemcpy(dmax, &mx, 4, hipMemcpyHostToDevice));
         CK(hipMemset(dst, 0, 4));
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k_gftt_select, dim3(1), dim3(SEL_THREADS), 0, 0, S);
+        hipLaunchKernelGGL(k_gftt_select, dim3(1), dim3(SEL_THREADS), lds, 0, S);
         CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         long long t[16];
