@@ -871,8 +871,10 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
     // dynamic LDS sized by the host (vo_gftt): page | accepted xy | grid (if it fits)
     extern __shared__ uint64_t sel_dyn[];
     uint64_t* page = sel_dyn;
-    uint32_t* acc_xy = (uint32_t*)(sel_dyn + PAGE);
+    uint32_t* cand_xy = (uint32_t*)(sel_dyn + PAGE);
+    uint32_t* acc_xy = cand_xy + PAGE;
     uint32_t* lgrid = acc_xy + P.acc_lds;
+    int* head = (int*)(lgrid + P.grid_lds);
     __shared__ uint32_t round_xy[64];
     __shared__ int hist[256];
     __shared__ int sh_int[16];
@@ -982,111 +984,259 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
             }
         }
         SELPROF(3);
-        // ---- greedy selection by wave 0, 64 candidates per round in sorted order.
-        // A candidate survives if no accepted corner in the 3x3 neighbouring cells is closer
-        // than minDistance (OpenCV's grid test).  Within a round, lane i additionally needs
-        // every earlier accepted lane j < i of the round to pass the same test; the lanes
-        // form a conflict mask against earlier tentative lanes, and wave-uniform scalar code
-        // walks the tentative lanes in order to pick the accepted set -- exactly OpenCV's
-        // sequential walk, without a ballot/shuffle round trip per accepted corner.
-        if (wave_id() == 0) {
-            const int lane = lane_id();
-            for (int s0 = 0; s0 < take && nacc < limit; s0 += 64) {
-                const int i = s0 + lane;
-                bool tent = i < take;
-                int x = 0, y = 0;
-                if (tent) {
-                    const uint32_t addr = (uint32_t)page[i];
-                    y = (int)(addr / (uint32_t)P.W);
-                    x = (int)(addr - (uint32_t)y * P.W);
-                }
+        const uint64_t page_last = page[take - 1];
+        if (use_grid && lds) {
+            // ---- exact parallel form of OpenCV's sequential minDistance walk.  Candidate i
+            // (rank order) is accepted iff no earlier accepted candidate in its 3x3 cell
+            // neighbourhood is closer than minDistance, and no corner accepted on an earlier
+            // page is.  Decisions only depend on earlier candidates, so they are resolved in
+            // parallel rounds (each round decides at least the lowest undecided candidate);
+            // the first `limit` accepted in rank order are the corners.
+            for (int i = tid; i < take; i += blockDim.x) {
+                const uint32_t addr = (uint32_t)page[i];
+                const int y = (int)(addr / (uint32_t)P.W), x = (int)(addr - (uint32_t)y * P.W);
+                cand_xy[i] = (uint32_t)x | ((uint32_t)y << 16);
+            }
+            for (int q = tid; q < gw * gh; q += blockDim.x) head[q] = -1;
+            __syncthreads();
+            int* nxt = (int*)page;                                // page keys are dead now
+            volatile uint8_t* stt = (volatile uint8_t*)(nxt + PAGE);
+            for (int i = tid; i < take; i += blockDim.x) {
+                const uint32_t xy = cand_xy[i];
+                const int x = (int)(xy & 0xFFFF), y = (int)(xy >> 16);
                 const int xc = x / cs, yc = y / cs;
-                if (tent && use_grid) {
+                bool rej = false;
+                if (nacc > 0) {
                     const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
                     const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
-                    for (int yy = y1; yy <= y2 && tent; ++yy)
-                        for (int xx = x1; xx <= x2 && tent; ++xx) {
-                            const uint32_t cv = cell_get(lds, lgrid, gg, yy * gw + xx);
+                    for (int yy = y1; yy <= y2; ++yy)
+                        for (int xx = x1; xx <= x2; ++xx) {
+                            const uint32_t cv = lgrid[yy * gw + xx];
                             for (int q = 0; q < 2; ++q) {
                                 const uint32_t id = (cv >> (16 * q)) & 0xFFFFu;
                                 if (id == 0xFFFFu) break;
-                                const uint32_t a = acc_xy[id];
-                                const float ddx = (float)x - (float)(a & 0xFFFF);
-                                const float ddy = (float)y - (float)(a >> 16);
-                                if ((double)(ddx * ddx + ddy * ddy) < md2) { tent = false; break; }
+                                const uint32_t aa = acc_xy[id];
+                                const float ddx = (float)x - (float)(aa & 0xFFFF);
+                                const float ddy = (float)y - (float)(aa >> 16);
+                                if ((double)(ddx * ddx + ddy * ddy) < md2) rej = true;
                             }
                         }
                 }
-                const uint64_t tmask = __ballot(tent);
-                if (tmask == 0) continue;
-                uint64_t amask = tmask;
-                if (use_grid) {
-                    // conflicts with earlier tentative lanes of this round
-                    round_xy[lane] = (uint32_t)x | ((uint32_t)y << 16);
+                stt[i] = rej ? 2 : 0;                             // 0 undecided, 1 accepted, 2 rejected
+                nxt[i] = atomicExch(&head[yc * gw + xc], i);
+            }
+            __syncthreads();
+            // each candidate's earlier conflicts (same test as OpenCV's walk), found once:
+            // count in LDS, indices in the per-chain scratch (the eigen-map buffer, unused on
+            // this path); more than CONF_K conflicts -> rescan the cells in every round
+            constexpr int CONF_K = 16;
+            uint16_t* conf = (uint16_t*)(P.gscratch + (int64_t)b * P.gstride);
+            uint8_t* ncf = (uint8_t*)(nxt + PAGE) + PAGE;          // PAGE bytes after stt
+            for (int i = tid; i < take; i += blockDim.x) {
+                if (stt[i] != 0) { ncf[i] = 0; continue; }
+                const uint32_t xy = cand_xy[i];
+                const int x = (int)(xy & 0xFFFF), y = (int)(xy >> 16);
+                const int xc = x / cs, yc = y / cs;
+                const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
+                const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
+                int c = 0;
+                for (int yy = y1; yy <= y2; ++yy)
+                    for (int xx = x1; xx <= x2; ++xx)
+                        for (int j = head[yy * gw + xx]; j >= 0; j = nxt[j]) {
+                            if (j >= i) continue;
+                            const uint32_t aa = cand_xy[j];
+                            const float ddx = (float)x - (float)(aa & 0xFFFF);
+                            const float ddy = (float)y - (float)(aa >> 16);
+                            if ((double)(ddx * ddx + ddy * ddy) < md2) {
+                                if (c < CONF_K) conf[(int64_t)i * CONF_K + c] = (uint16_t)j;
+                                ++c;
+                            }
+                        }
+                ncf[i] = (uint8_t)min(c, 255);
+            }
+            __syncthreads();
+            SELPROF(5);
+            for (;;) {
+                if (tid == 0) sh_int[3] = 0;
+                __syncthreads();
+                bool changed = false;
+                for (int i = tid; i < take; i += blockDim.x) {
+                    if (stt[i] != 0) continue;
+                    bool blocked = false, rej = false;
+                    const int c = ncf[i];
+                    if (c <= CONF_K) {
+                        for (int k = 0; k < c; ++k) {
+                            const uint8_t sj = stt[conf[(int64_t)i * CONF_K + k]];
+                            if (sj == 1) { rej = true; break; }
+                            if (sj == 0) blocked = true;
+                        }
+                    } else {
+                        const uint32_t xy = cand_xy[i];
+                        const int x = (int)(xy & 0xFFFF), y = (int)(xy >> 16);
+                        const int xc = x / cs, yc = y / cs;
+                        const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
+                        const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
+                        for (int yy = y1; yy <= y2 && !rej; ++yy)
+                            for (int xx = x1; xx <= x2 && !rej; ++xx)
+                                for (int j = head[yy * gw + xx]; j >= 0; j = nxt[j]) {
+                                    if (j >= i) continue;
+                                    const uint8_t sj = stt[j];
+                                    if (sj == 2) continue;
+                                    const uint32_t aa = cand_xy[j];
+                                    const float ddx = (float)x - (float)(aa & 0xFFFF);
+                                    const float ddy = (float)y - (float)(aa >> 16);
+                                    if ((double)(ddx * ddx + ddy * ddy) < md2) {
+                                        if (sj == 1) { rej = true; break; }
+                                        blocked = true;
+                                    }
+                                }
+                    }
+                    if (rej) { stt[i] = 2; changed = true; }
+                    else if (!blocked) { stt[i] = 1; changed = true; }
+                }
+                if (changed) sh_int[3] = 1;
+                __syncthreads();
+                const int any = sh_int[3];
+                __syncthreads();
+#ifdef VO_SELECT_PROF
+                if (tid == 0 && blockIdx.x == 0) g_selprof[10]++;
+#endif
+                if (!any) break;
+            }
+            SELPROF(6);
+            // accepted candidates in rank order -> corners (up to limit) and the grid
+            for (int base = 0; base < take && nacc < limit; base += blockDim.x) {
+                const int i = base + tid;
+                const bool acc = i < take && stt[i] == 1;
+                int tot;
+                const int pos = nacc + block_scan_flag(acc, sh_int, &tot);
+                if (acc && pos < limit) {
+                    const uint32_t xy = cand_xy[i];
+                    const int x = (int)(xy & 0xFFFF), y = (int)(xy >> 16);
+                    acc_xy[pos] = xy;
+                    out[2 * pos] = (float)x;
+                    out[2 * pos + 1] = (float)y;
+                    // at most two corners share a cell; slot order inside a cell is irrelevant
+                    const int cell = (y / cs) * gw + (x / cs);
+                    uint32_t cur = lgrid[cell];
+                    for (;;) {
+                        const uint32_t nv = ((cur & 0xFFFFu) == 0xFFFFu) ? ((cur & 0xFFFF0000u) | (uint32_t)pos)
+                                                                        : ((cur & 0xFFFFu) | ((uint32_t)pos << 16));
+                        const uint32_t prev = atomicCAS(&lgrid[cell], cur, nv);
+                        if (prev == cur) break;
+                        cur = prev;
+                    }
+                }
+                nacc = min(nacc + tot, limit);
+            }
+            if (tid == 0) sh_int[2] = nacc;
+        } else {
+        // ---- greedy selection by wave 0, 64 candidates per round in sorted order.
+            // A candidate survives if no accepted corner in the 3x3 neighbouring cells is closer
+            // than minDistance (OpenCV's grid test).  Within a round, lane i additionally needs
+            // every earlier accepted lane j < i of the round to pass the same test; the lanes
+            // form a conflict mask against earlier tentative lanes, and wave-uniform scalar code
+            // walks the tentative lanes in order to pick the accepted set -- exactly OpenCV's
+            // sequential walk, without a ballot/shuffle round trip per accepted corner.
+            if (wave_id() == 0) {
+                const int lane = lane_id();
+                for (int s0 = 0; s0 < take && nacc < limit; s0 += 64) {
+                    const int i = s0 + lane;
+                    bool tent = i < take;
+                    int x = 0, y = 0;
+                    if (tent) {
+                        const uint32_t addr = (uint32_t)page[i];
+                        y = (int)(addr / (uint32_t)P.W);
+                        x = (int)(addr - (uint32_t)y * P.W);
+                    }
+                    const int xc = x / cs, yc = y / cs;
+                    if (tent && use_grid) {
+                        const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
+                        const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
+                        for (int yy = y1; yy <= y2 && tent; ++yy)
+                            for (int xx = x1; xx <= x2 && tent; ++xx) {
+                                const uint32_t cv = cell_get(lds, lgrid, gg, yy * gw + xx);
+                                for (int q = 0; q < 2; ++q) {
+                                    const uint32_t id = (cv >> (16 * q)) & 0xFFFFu;
+                                    if (id == 0xFFFFu) break;
+                                    const uint32_t a = acc_xy[id];
+                                    const float ddx = (float)x - (float)(a & 0xFFFF);
+                                    const float ddy = (float)y - (float)(a >> 16);
+                                    if ((double)(ddx * ddx + ddy * ddy) < md2) { tent = false; break; }
+                                }
+                            }
+                    }
+                    const uint64_t tmask = __ballot(tent);
+                    if (tmask == 0) continue;
+                    uint64_t amask = tmask;
+                    if (use_grid) {
+                        // conflicts with earlier tentative lanes of this round
+                        round_xy[lane] = (uint32_t)x | ((uint32_t)y << 16);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        uint32_t clo = 0, chi = 0;
+                        uint64_t rest = tmask & ((1ull << lane) - 1ull) & (tent ? ~0ull : 0ull);
+                        // uniform walk over the tentative lanes; each lane keeps the earlier ones
+                        for (uint64_t m = tmask; m; m &= m - 1) {
+                            const int j = __builtin_ctzll(m);
+                            if (!((rest >> j) & 1ull)) continue;
+                            const uint32_t a = round_xy[j];
+                            const int tx = (int)(a & 0xFFFF), ty = (int)(a >> 16);
+                            if (abs(tx / cs - xc) <= 1 && abs(ty / cs - yc) <= 1) {
+                                const float ddx = (float)x - (float)tx, ddy = (float)y - (float)ty;
+                                if ((double)(ddx * ddx + ddy * ddy) < md2) {
+                                    if (j < 32) clo |= 1u << j; else chi |= 1u << (j - 32);
+                                }
+                            }
+                        }
+                        // in-order resolution on scalar registers
+                        amask = 0;
+                        for (uint64_t m = tmask; m; m &= m - 1) {
+                            const int j = __builtin_ctzll(m);
+                            const uint64_t cj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)clo, j) |
+                                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)chi, j) << 32);
+                            if ((cj & amask) == 0) amask |= 1ull << j;
+                        }
+                    }
+                    // respect maxCorners: keep the first (limit - nacc) accepted lanes
+                    int nnew = __popcll(amask);
+                    if (nnew > limit - nacc) {
+                        uint64_t m = amask, keep = 0;
+                        for (int c = 0; c < limit - nacc; ++c) { const uint64_t lb = m & (~m + 1ull); keep |= lb; m ^= lb; }
+                        amask = keep;
+                        nnew = limit - nacc;
+                    }
+                    if ((amask >> lane) & 1ull) {
+                        const int idx = nacc + __popcll(amask & ((1ull << lane) - 1ull));
+                        acc_xy[idx] = (uint32_t)x | ((uint32_t)y << 16);
+                        out[2 * idx] = (float)x;
+                        out[2 * idx + 1] = (float)y;
+                        if (use_grid) {
+                            // at most two corners share a cell; slot order inside a cell is irrelevant
+                            const int cell = yc * gw + xc;
+                            uint32_t cur = cell_get(lds, lgrid, gg, cell);
+                            for (;;) {
+                                const uint32_t nv = ((cur & 0xFFFFu) == 0xFFFFu) ? ((cur & 0xFFFF0000u) | (uint32_t)idx)
+                                                                                : ((cur & 0xFFFFu) | ((uint32_t)idx << 16));
+                                const uint32_t prev = lds ? atomicCAS(&lgrid[cell], cur, nv) : atomicCAS(&gg[cell], cur, nv);
+                                if (prev == cur) break;
+                                cur = prev;
+                            }
+                        }
+                    }
+                    nacc += nnew;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    uint32_t clo = 0, chi = 0;
-                    uint64_t rest = tmask & ((1ull << lane) - 1ull) & (tent ? ~0ull : 0ull);
-                    // uniform walk over the tentative lanes; each lane keeps the earlier ones
-                    for (uint64_t m = tmask; m; m &= m - 1) {
-                        const int j = __builtin_ctzll(m);
-                        if (!((rest >> j) & 1ull)) continue;
-                        const uint32_t a = round_xy[j];
-                        const int tx = (int)(a & 0xFFFF), ty = (int)(a >> 16);
-                        if (abs(tx / cs - xc) <= 1 && abs(ty / cs - yc) <= 1) {
-                            const float ddx = (float)x - (float)tx, ddy = (float)y - (float)ty;
-                            if ((double)(ddx * ddx + ddy * ddy) < md2) {
-                                if (j < 32) clo |= 1u << j; else chi |= 1u << (j - 32);
-                            }
-                        }
-                    }
-                    // in-order resolution on scalar registers
-                    amask = 0;
-                    for (uint64_t m = tmask; m; m &= m - 1) {
-                        const int j = __builtin_ctzll(m);
-                        const uint64_t cj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)clo, j) |
-                                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)chi, j) << 32);
-                        if ((cj & amask) == 0) amask |= 1ull << j;
-                    }
                 }
-                // respect maxCorners: keep the first (limit - nacc) accepted lanes
-                int nnew = __popcll(amask);
-                if (nnew > limit - nacc) {
-                    uint64_t m = amask, keep = 0;
-                    for (int c = 0; c < limit - nacc; ++c) { const uint64_t lb = m & (~m + 1ull); keep |= lb; m ^= lb; }
-                    amask = keep;
-                    nnew = limit - nacc;
-                }
-                if ((amask >> lane) & 1ull) {
-                    const int idx = nacc + __popcll(amask & ((1ull << lane) - 1ull));
-                    acc_xy[idx] = (uint32_t)x | ((uint32_t)y << 16);
-                    out[2 * idx] = (float)x;
-                    out[2 * idx + 1] = (float)y;
-                    if (use_grid) {
-                        // at most two corners share a cell; slot order inside a cell is irrelevant
-                        const int cell = yc * gw + xc;
-                        uint32_t cur = cell_get(lds, lgrid, gg, cell);
-                        for (;;) {
-                            const uint32_t nv = ((cur & 0xFFFFu) == 0xFFFFu) ? ((cur & 0xFFFF0000u) | (uint32_t)idx)
-                                                                            : ((cur & 0xFFFFu) | ((uint32_t)idx << 16));
-                            const uint32_t prev = lds ? atomicCAS(&lgrid[cell], cur, nv) : atomicCAS(&gg[cell], cur, nv);
-                            if (prev == cur) break;
-                            cur = prev;
-                        }
-                    }
-                }
-                nacc += nnew;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane == 0) sh_int[2] = nacc;
             }
-            if (lane == 0) sh_int[2] = nacc;
         }
         __syncthreads();
         SELPROF(4);
         nacc = sh_int[2];
-        upper = page[take - 1];
+        upper = page_last;
         has_upper = true;
         remaining -= take;
         __syncthreads();
@@ -1270,10 +1420,12 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
         const int64_t cells = md >= 1 ? (int64_t)((d->W + cs - 1) / cs) * ((d->H + cs - 1) / cs) : 0;
         S.acc_lds = d->mcap < ACC_MAX ? d->mcap : ACC_MAX;
         S.grid_lds = cells <= GRID_LDS_CELLS ? (int)cells : 0;
-        const size_t lds = 8 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 4 * (size_t)S.grid_lds;
+        // grid + per-cell candidate lists in LDS when they fit, else the L2 grid path
+        if (12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds > 150 * 1024) S.grid_lds = 0;
+        const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
         static const bool attr_ok = hipFuncSetAttribute((const void*)k_gftt_select,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        8 * PAGE + 4 * ACC_MAX + 4 * GRID_LDS_CELLS) == hipSuccess;
+                                                        150 * 1024) == hipSuccess;
         if (!attr_ok && lds > 64 * 1024) return VO_EHIP;
         hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), lds, st, S);
     }
