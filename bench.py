@@ -226,14 +226,15 @@ def main():
     torch.cuda.synchronize()
 
     nst = len(Engine.STAGES)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(nst + 1)] for _ in range(K_steps)]
+    # (start, end) HIP events per stage and step, recorded on the stream each stage runs on
+    ev = [[[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(nst)] for _ in range(K_steps)]
 
     barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(K_steps):
         e = ev[k]
-        step_all(2 + W_steps + k, marks=lambda i, e=e: e[i].record())
+        step_all(2 + W_steps + k, marks=lambda i, end, strm, e=e: e[i][int(end)].record(strm))
     host_s = time.perf_counter() - t_start          # launch-side time (no sync inside steps)
     torch.cuda.synchronize()
     barrier()
@@ -248,7 +249,7 @@ def main():
     st_ms = np.zeros(nst)
     for k in range(K_steps):
         for i in range(nst):
-            st_ms[i] += ev[k][i].elapsed_time(ev[k][i + 1])
+            st_ms[i] += ev[k][i][0].elapsed_time(ev[k][i][1])
     st_ms /= max(1, K_steps)
 
     # live point counts of the last step (for the KLT algorithmic bytes)

@@ -43,8 +43,15 @@ class VisualOdometryPipeLine:
         self._boot_done = False
 
     # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _as_frame(img):
+        """numpy image (as the reference passes, utils.py:55-81) or a uint8 torch tensor
+        already on the device (no host round trip)."""
+        import torch
+        return img if isinstance(img, torch.Tensor) else np.asarray(img)
+
     def _engine_for(self, img):
-        h, w = np.asarray(img).shape[:2]
+        h, w = tuple(img.shape[:2])
         if self._eng is None or (self._eng.W, self._eng.H) != (w, h):
             nc, pc, fc = self._caps
             self._eng = Engine(self.K, self.options, w, h, batch=1, device=self._device, ncap=nc, pcap=pc, fcap=fc)
@@ -68,9 +75,10 @@ class VisualOdometryPipeLine:
 
     # ------------------------------------------------------------------ API
     def initialization(self, img0, img1):
+        img0, img1 = self._as_frame(img0), self._as_frame(img1)
         eng = self._engine_for(img1)
-        eng.bootstrap(np.asarray(img0)[None], np.asarray(img1)[None])
-        self._frame = np.asarray(img1)
+        eng.bootstrap(img0[None], img1[None])
+        self._frame = img1
         self._boot_done = True
         self._raise_status(self._status())
 
@@ -78,11 +86,12 @@ class VisualOdometryPipeLine:
         if not self._boot_done:
             raise RuntimeError("initialization() must run first")
         eng = self._eng
+        img = self._as_frame(img)
         if self._use_graph:
-            eng.step_graph(np.asarray(img)[None])
+            eng.step_graph(img[None])
         else:
-            eng.step(np.asarray(img)[None])
-        self._frame = np.asarray(img)
+            eng.step(img[None])
+        self._frame = img
         st = self._status()
         if st == L.ST_OK:
             n_inl = int(eng.t["nInl"][0])

@@ -844,7 +844,7 @@ struct SelParams {
     int acc_lds;             // accepted-corner slots in LDS (min(mcap, ACC_MAX))
     int grid_lds;            // grid cells held in LDS (0: grid in L2)
     int64_t gstride;
-    int32_t* chain_status;
+    const int32_t* chain_status;
 };
 
 // A grid cell holds up to two accepted-corner indices (u16 each, 0xFFFF = empty); the
@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
     SELPROF(0);
     const int nk_all = P.nkeys[b];
     if (nk_all > P.ccap) {
-        if (tid == 0) P.chain_status[b] = VO_ST_CAPACITY;
+        if (tid == 0) P.ncorners[b] = -1;          // capacity: k_add_finish raises it
         return;
     }
     // quality gate of goodFeaturesToTrack: v > quality * max(eig)  (featureselect.cpp);
@@ -1242,9 +1242,10 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
         __syncthreads();
     }
     if (tid == 0) {
-        P.ncorners[b] = nacc;
-        // more corners wanted than this engine can hold -> never truncate silently
-        if (nacc == cap && cap < want && remaining > 0) P.chain_status[b] = VO_ST_CAPACITY;
+        // more corners wanted than this engine can hold -> never truncate silently.  The
+        // status word is not written here: GFTT runs on a side stream concurrently with PnP,
+        // which owns it; k_add_finish turns ncorners < 0 into VO_ST_CAPACITY.
+        P.ncorners[b] = (nacc == cap && cap < want && remaining > 0) ? -1 : nacc;
     }
 }
 

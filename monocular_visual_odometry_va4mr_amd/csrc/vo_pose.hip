@@ -786,6 +786,7 @@ __global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
     if (s.status[b] != 0) return;
     const int nF = s.nF[b];
     const int M = s.nCorners[b];
+    if (M < 0) { if (tid == 0) s.status[b] = VO_ST_CAPACITY; return; }      // k_gftt_select overflow
     if (M == 0) { if (tid == 0) s.status[b] = VO_ST_GFTT_NONE; return; }   // None.squeeze()
     if (M == 1) { if (tid == 0) s.status[b] = VO_ST_GFTT_ONE; return; }    // (2,) indexing
     const int P = s.nC[b];

@@ -184,32 +184,50 @@ class Engine:
     def step(self, frames, marks=None):
         """One continuous_operation for every chain (frames: uint8 [B,H,W], any device).
 
-        ``marks``: optional callable invoked with the stage index before each stage and
-        with len(STAGES) after the last one (bench.py records HIP events there)."""
+        ``marks``: optional callable ``marks(stage_index, end, stream)`` invoked on the
+        launching thread right before (end=False) and after (end=True) each stage, with
+        the torch stream that stage runs on (bench.py records HIP events there)."""
         frames = self._frames(frames)
         self._step_launch(frames, self.prev, marks)
         self.prev = 1 - self.prev
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def _step_launch(self, frames, prev, marks=None):
+        """Stage DAG of one step on two streams.  main: pyramid(cur) -> track(prev) -> PnP ->
+        triangulate -> [join] -> add_finish.  side: GFTT on the new frame (needs only its
+        pyramid, VisualOdometryPipeLine.py:253) and, once tracking has read the previous
+        frame's derivatives, the new frame's Scharr derivatives -- both overlap PnP.  GFTT
+        never writes the chain status (PnP owns it while the two run; see k_gftt_select)."""
         cur = 1 - prev
-        lib, st = self.lib, self.stream
+        lib = self.lib
+        main = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        sm, ss = C.c_void_p(main.cuda_stream), C.c_void_p(side.cuda_stream)
         pd, po, ps = self._pd, self._po, self._ps
         fp = C.c_void_p(frames.data_ptr())
-        calls = (
-            lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, st),
-            lambda: lib.vo_track(pd, po, ps, prev, st),
-            lambda: lib.vo_pyr_deriv(pd, ps, cur, st),
-            lambda: lib.vo_pnp(pd, po, ps, st),
-            lambda: lib.vo_triangulate(pd, po, ps, 0, st),
-            lambda: lib.vo_gftt(pd, po, ps, cur, st),
-            lambda: lib.vo_add_corners_finish(pd, po, ps, st),
-        )
-        for i, (name, call) in enumerate(zip(self.STAGES, calls)):
+        names = self.STAGES
+
+        def run(i, strm, call):
             if marks is not None:
-                marks(i)
-            self._chk(call(), "vo_" + name)
-        if marks is not None:
-            marks(len(calls))
+                marks(i, False, strm)
+            self._chk(call(), "vo_" + names[i])
+            if marks is not None:
+                marks(i, True, strm)
+
+        run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
+        side.wait_stream(main)                                    # pyramid(cur) ready
+        run(5, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
+        run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
+        side.wait_stream(main)                                    # der(prev) consumed
+        run(2, side, lambda: lib.vo_pyr_deriv(pd, ps, cur, ss))
+        run(3, main, lambda: lib.vo_pnp(pd, po, ps, sm))
+        run(4, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
+        main.wait_stream(side)                                    # corners + der(cur) ready
+        run(6, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))
 
     def capture_step(self):
         """Capture the two ping-pong variants of the step into hipGraphs; returns a
