@@ -216,23 +216,21 @@ VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
                 cs[3 * q + 2] = f;
             }
             wave_lds_sync();
-            for (int q = 0; q < NP; ++q) {
+            // the NP rotations touch disjoint column pairs: apply them all at once, one
+            // (pair, row of A or V) item per lane
+#pragma unroll
+            for (int q = 0; q < NP; ++q) changed |= cs[3 * q + 2] != 0.0;
+            for (int it = lane; it < NP * (M + N); it += 64) {
+                const int q = it / (M + N), row = it - q * (M + N);
                 if (cs[3 * q + 2] == 0.0) continue;
-                changed = true;
                 const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
                 const int b = ((N - 2 - q + r) % (N - 1)) + 1;
                 const int i = a < b ? a : b, j = a < b ? b : a;
                 const double c = cs[3 * q], s = cs[3 * q + 1];
-                if (lane < M) {
-                    double ai = A[lane * N + i], aj = A[lane * N + j];
-                    A[lane * N + i] = c * ai - s * aj;
-                    A[lane * N + j] = s * ai + c * aj;
-                }
-                if (lane < N) {
-                    double vi = V[lane * N + i], vj = V[lane * N + j];
-                    V[lane * N + i] = c * vi - s * vj;
-                    V[lane * N + j] = s * vi + c * vj;
-                }
+                double* X = row < M ? A + row * N : V + (row - M) * N;
+                const double xi = X[i], xj = X[j];
+                X[i] = c * xi - s * xj;
+                X[j] = s * xi + c * xj;
             }
             wave_lds_sync();
         }
@@ -587,6 +585,57 @@ VO_DEV void p3p_reproject_input(const CamK& k, double u, double v, double* uo, d
     float vn = (float)((v - k.cy) * k.ify);
     *uo = (double)un * k.fx + k.cx;
     *vo = (double)vn * k.fy + k.cy;
+}
+
+// Solution `sol` of a 4-point P3P, for the lane-per-solution layout of k_pnp_ransac: the
+// same bearing/length computation as p3p_solve4 (every lane of a hypothesis runs it on the
+// same data), then one align_horn.  Returns 0 when the quartic gave fewer solutions;
+// otherwise R, T and the 4th-point error e that p3p_solve4 ranks the solutions by.
+VO_DEV int p3p_solution(const CamK& k, const double* obj, const double* img_px, int sol, double* R, double* T,
+                        double* e)
+{
+    double mu[4], mv[4], mk[3];
+    for (int i = 0; i < 4; ++i) {
+        double u, v;
+        p3p_reproject_input(k, img_px[2 * i], img_px[2 * i + 1], &u, &v);
+        mu[i] = k.ifx * u - k.cx_fx;
+        mv[i] = k.ify * v - k.cy_fx;
+    }
+    for (int i = 0; i < 3; ++i) {
+        double nrm = sqrt(mu[i] * mu[i] + mv[i] * mv[i] + 1);
+        mk[i] = 1. / nrm;
+        mu[i] *= mk[i];
+        mv[i] *= mk[i];
+    }
+    const double* X = obj;
+    double dist[3], cs[3];
+    dist[0] = sqrt((X[3] - X[6]) * (X[3] - X[6]) + (X[4] - X[7]) * (X[4] - X[7]) + (X[5] - X[8]) * (X[5] - X[8]));
+    dist[1] = sqrt((X[0] - X[6]) * (X[0] - X[6]) + (X[1] - X[7]) * (X[1] - X[7]) + (X[2] - X[8]) * (X[2] - X[8]));
+    dist[2] = sqrt((X[0] - X[3]) * (X[0] - X[3]) + (X[1] - X[4]) * (X[1] - X[4]) + (X[2] - X[5]) * (X[2] - X[5]));
+    cs[0] = mu[1] * mu[2] + mv[1] * mv[2] + mk[1] * mk[2];
+    cs[1] = mu[0] * mu[2] + mv[0] * mv[2] + mk[0] * mk[2];
+    cs[2] = mu[0] * mu[1] + mv[0] * mv[1] + mk[0] * mk[1];
+    double L[4][3];
+    const int n = p3p_lengths(L, dist, cs);
+    if (sol >= n) return 0;
+    double l0 = 0, l1 = 0, l2 = 0;          // L[sol] selected with constant indices
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i == sol) { l0 = L[i][0]; l1 = L[i][1]; l2 = L[i][2]; }
+    const double ls[3] = {l0, l1, l2};
+    double M[3][3], P[3][3];
+    for (int j = 0; j < 3; ++j) {
+        M[j][0] = ls[j] * mu[j];
+        M[j][1] = ls[j] * mv[j];
+        M[j][2] = ls[j] * mk[j];
+        P[j][0] = X[3 * j]; P[j][1] = X[3 * j + 1]; P[j][2] = X[3 * j + 2];
+    }
+    align_horn(M, P, R, T);
+    double X3 = R[0] * X[9] + R[1] * X[10] + R[2] * X[11] + T[0];
+    double Y3 = R[3] * X[9] + R[4] * X[10] + R[5] * X[11] + T[1];
+    double Z3 = R[6] * X[9] + R[7] * X[10] + R[8] * X[11] + T[2];
+    *e = (X3 / Z3 - mu[3]) * (X3 / Z3 - mu[3]) + (Y3 / Z3 - mv[3]) * (Y3 / Z3 - mv[3]);
+    return 1;
 }
 
 // 4-point P3P (solvePnP SOLVEPNP_P3P): obj 4x3, img_px 4x2 (doubles from float inputs)

@@ -190,55 +190,53 @@ VO_DEV void epnp_mtm_part(int n, const double* alphas, const double* us, double 
     }
 }
 
-// compute_R_and_t for approximation `a` (all threads participate)
-VO_DEV void epnp_R_and_t(EpnpShared& S, int a, const double* K, const double* pws, const double* us,
-                         const double* alphas, double* pcs, int n)
+// compute_R_and_t for approximation `a`, executed by one whole wave (the three
+// approximations run on waves 0..2 at once).  The camera-frame points pcs are recomputed
+// from alphas and ccs where needed instead of being stored (same products and sums; the
+// sign flip negates ccs, which negates every pcs exactly).  S.pw0 is set by the caller.
+VO_DEV void epnp_R_and_t_wave(EpnpShared& S, int a, const double* K, const double* pws, const double* us,
+                              const double* alphas, int n)
 {
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        for (int j = 0; j < 4; ++j) for (int k = 0; k < 3; ++k) S.ccs[j][k] = 0;
-        for (int i = 0; i < 4; ++i) {
-            int col = 11 - i;
-            for (int j = 0; j < 4; ++j)
-                for (int k = 0; k < 3; ++k) S.ccs[j][k] += S.betas[a][i] * S.V12[(3 * j + k) * 12 + col];
-        }
+    const int lane = lane_id();
+    double* tmp = S.tmp + 24 * (a - 1);
+    double ccs[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ccs[j][k] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int col = 11 - i;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ccs[j][k] += S.betas[a][i] * S.V12[(3 * j + k) * 12 + col];
     }
-    __syncthreads();
-    for (int i = tid; i < n; i += blockDim.x) {
+    auto pc = [&](int i, int j) {
         const double* al = alphas + 4 * i;
+        return al[0] * ccs[0][j] + al[1] * ccs[1][j] + al[2] * ccs[2][j] + al[3] * ccs[3][j];
+    };
+    if (pc(0, 2) < 0.0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ccs[j][k] = -ccs[j][k];
+    }
+    wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pc(i, 0); c[1] = pc(i, 1); c[2] = pc(i, 2); }, tmp);
+    wave_lds_sync();
+    double pc0[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pc0[j] = tmp[j] / n;
+    wave_lds_sync();
+    wave_det_sum<9>(n, [&](int i, double* c) {
+        double p[3] = {pc(i, 0), pc(i, 1), pc(i, 2)};
         for (int j = 0; j < 3; ++j)
-            pcs[3 * i + j] = al[0] * S.ccs[0][j] + al[1] * S.ccs[1][j] + al[2] * S.ccs[2][j] + al[3] * S.ccs[3][j];
-    }
-    __syncthreads();
-    if (tid == 0) S.flip = pcs[2] < 0.0;
-    __syncthreads();
-    if (S.flip) {
-        if (tid == 0) for (int j = 0; j < 4; ++j) for (int k = 0; k < 3; ++k) S.ccs[j][k] = -S.ccs[j][k];
-        for (int i = tid; i < 3 * n; i += blockDim.x) pcs[i] = -pcs[i];
-    }
-    __syncthreads();
-    if (wave_id() == 0) {
-        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pcs[3 * i]; c[1] = pcs[3 * i + 1]; c[2] = pcs[3 * i + 2]; }, S.tmp);
-    }
-    __syncthreads();
-    if (tid == 0) for (int j = 0; j < 3; ++j) S.pc0[j] = S.tmp[j] / n;
-    __syncthreads();
-    if (wave_id() == 0) {
-        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp);
-    }
-    __syncthreads();
-    if (tid == 0) for (int j = 0; j < 3; ++j) S.pw0[j] = S.tmp[j] / n;
-    __syncthreads();
-    if (wave_id() == 0) {
-        wave_det_sum<9>(n, [&](int i, double* c) {
-            for (int j = 0; j < 3; ++j)
-                for (int k = 0; k < 3; ++k) c[j * 3 + k] = (pcs[3 * i + j] - S.pc0[j]) * (pws[3 * i + k] - S.pw0[k]);
-        }, S.tmp);
-    }
-    __syncthreads();
-    if (tid == 0) {
+            for (int k = 0; k < 3; ++k) c[j * 3 + k] = (p[j] - pc0[j]) * (pws[3 * i + k] - S.pw0[k]);
+    }, tmp);
+    wave_lds_sync();
+    if (lane == 0) {
         double abt[9], w[3], V[9];
-        for (int q = 0; q < 9; ++q) abt[q] = S.tmp[q];
+        for (int q = 0; q < 9; ++q) abt[q] = tmp[q];
         svd_jacobi<3, 3>(abt, w, V);
         double* R = S.Rs[a];
         for (int i = 0; i < 3; ++i)
@@ -246,10 +244,10 @@ VO_DEV void epnp_R_and_t(EpnpShared& S, int a, const double* K, const double* pw
                 R[i * 3 + j] = abt[i * 3 + 0] * V[j * 3 + 0] + abt[i * 3 + 1] * V[j * 3 + 1] + abt[i * 3 + 2] * V[j * 3 + 2];
         if (det3(R) < 0) { R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8]; }
         for (int i = 0; i < 3; ++i)
-            S.ts[a][i] = S.pc0[i] - (R[i * 3] * S.pw0[0] + R[i * 3 + 1] * S.pw0[1] + R[i * 3 + 2] * S.pw0[2]);
+            S.ts[a][i] = pc0[i] - (R[i * 3] * S.pw0[0] + R[i * 3 + 1] * S.pw0[1] + R[i * 3 + 2] * S.pw0[2]);
     }
-    __syncthreads();
-    if (wave_id() == 0) {
+    wave_lds_sync();
+    {
         const double* R = S.Rs[a];
         const double* t = S.ts[a];
         const double fu = K[0], fv = K[4], uc = K[2], vc = K[5];
@@ -262,11 +260,10 @@ VO_DEV void epnp_R_and_t(EpnpShared& S, int a, const double* K, const double* pw
             double ve = vc + fv * Yc * inv_Zc;
             double u = us[2 * i], v = us[2 * i + 1];
             c[0] = sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
-        }, S.tmp);
+        }, tmp);
     }
-    __syncthreads();
-    if (tid == 0) S.rep[a] = S.tmp[0] / n;
-    __syncthreads();
+    wave_lds_sync();
+    if (lane == 0) S.rep[a] = tmp[0] / n;
 }
 
 // EPnP (epnp::compute_pose), all threads of the block; n >= 4
@@ -388,7 +385,13 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
     PNPPROF(12);
     // the oracle runs approximation 1's R,t before computing approximation 2's betas; the
     // betas do not depend on R,t, so computing all betas first is equivalent
-    for (int a = 1; a <= 3; ++a) epnp_R_and_t(S, a, K, pws, us, alphas, pcs, n);
+    if (wave_id() == 0)
+        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp + 72);
+    __syncthreads();
+    if (tid == 0) for (int j = 0; j < 3; ++j) S.pw0[j] = S.tmp[72 + j] / n;
+    __syncthreads();
+    if (wave_id() < 3) epnp_R_and_t_wave(S, wave_id() + 1, K, pws, us, alphas, n);
+    __syncthreads();
     PNPPROF(13);
     if (tid == 0) {
         int N = 1;
@@ -402,6 +405,9 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
 
 // ------------------------------------------------------------------ PnP-RANSAC
 #define HYP 64
+#ifndef VO_PNP_CH1
+#define VO_PNP_CH1 32
+#endif
 
 struct PnPArgs {
     double K[9];
@@ -471,9 +477,9 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         const int it0 = sh[0];
         const int niters0 = sh[1];
         if (it0 >= niters0) break;
-        // a small first round: with the usual inlier ratios the adaptive iteration count
-        // drops below 16 there, and fewer diverging P3P lanes finish sooner
-        const int CH = it0 == 0 ? HYP / 4 : HYP;
+        // a smaller first round: with the usual inlier ratios the adaptive iteration count
+        // drops below it there, and fewer diverging P3P lanes and inlier counts finish sooner
+        const int CH = it0 == 0 ? VO_PNP_CH1 : HYP;
         PNPPROF(1);
         if (tid == 0) {
             for (int h = 0; h < CH; ++h) {
@@ -489,19 +495,35 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
             }
         }
         __syncthreads();
-        if (tid < CH) {
-            const int h = tid;
-            double o[12], im[8], R[9], t[3];
-            for (int j = 0; j < 4; ++j) {
-                const int id = sub[h][j];
-                o[3 * j] = obj[3 * id]; o[3 * j + 1] = obj[3 * id + 1]; o[3 * j + 2] = obj[3 * id + 2];
-                im[2 * j] = img[2 * id]; im[2 * j + 1] = img[2 * id + 1];
+        {
+            // four lanes per hypothesis, one P3P solution each (p3p_solution); the lanes then
+            // apply p3p_solve4's rule (first solution with a strictly smaller 4th-point error)
+            const int h = tid >> 2, sol = tid & 3, lane = lane_id();
+            double R[9], t[3], e = 0.0;
+            int ok = 0;
+            if (h < CH && it0 + h < niters0) {
+                double o[12], im[8];
+                for (int j = 0; j < 4; ++j) {
+                    const int id = sub[h][j];
+                    o[3 * j] = obj[3 * id]; o[3 * j + 1] = obj[3 * id + 1]; o[3 * j + 2] = obj[3 * id + 2];
+                    im[2 * j] = img[2 * id]; im[2 * j + 1] = img[2 * id + 1];
+                }
+                ok = p3p_solution(k, o, im, sol, R, t, &e);
             }
-            const int ok = (it0 + h < niters0) ? p3p_solve4(k, o, im, R, t) : 0;
-            valid[h] = ok;
-            if (ok) {
-                for (int q = 0; q < 9; ++q) mdl[h][q] = R[q];
-                for (int q = 0; q < 3; ++q) mdl[h][9 + q] = t[q];
+            int bsol = -1;
+            double be = 0.0;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int oks = __shfl(ok, (lane & ~3) | s2, 64);
+                const double es = __shfl(e, (lane & ~3) | s2, 64);
+                if (oks && (bsol < 0 || es < be)) { bsol = s2; be = es; }
+            }
+            if (h < CH) {
+                if (sol == 0) valid[h] = bsol >= 0;
+                if (sol == bsol) {
+                    for (int q = 0; q < 9; ++q) mdl[h][q] = R[q];
+                    for (int q = 0; q < 3; ++q) mdl[h][9 + q] = t[q];
+                }
             }
         }
         __syncthreads();

@@ -46,10 +46,53 @@ __global__ void __launch_bounds__(256) k_t_epnp(const double* K, const double* p
     if (threadIdx.x == 0) { t[0] = c1 - c0; for (int i = 0; i < 9; ++i) out[i] = R[i]; }
 }
 
+
+// P3P pieces on lane 0 (wall clock, 100 MHz) and the 64-lane layouts of k_pnp_ransac
+__global__ void k_t_p3p_parts(const double* K, const double* pws, const double* us, int n, long long* t)
+{
+    vg::CamK k = vg::camk(K);
+    const int lane = threadIdx.x;
+    double o[12], im[8], R[9], T[3], e;
+    auto load = [&](int h) {
+        for (int j = 0; j < 4; ++j) {
+            const int id = (h * 37 + j * 101 + 5) % n;
+            for (int q = 0; q < 3; ++q) o[3 * j + q] = pws[3 * id + q];
+            for (int q = 0; q < 2; ++q) im[2 * j + q] = us[2 * id + q];
+        }
+    };
+    // lane 0 alone: lengths (quartic) then one align
+    if (lane == 0) {
+        load(0);
+        double dist[3] = {1.0, 1.2, 0.9}, cs[3] = {0.99, 0.98, 0.985}, L[4][3];
+        long long a0 = wall_clock64();
+        int ns = vg::p3p_lengths(L, dist, cs);
+        long long a1 = wall_clock64();
+        int ok = vg::p3p_solution(k, o, im, 0, R, T, &e);
+        long long a2 = wall_clock64();
+        int ok2 = vg::p3p_solve4(k, o, im, R, T);
+        long long a3 = wall_clock64();
+        t[0] = a1 - a0; t[1] = a2 - a1; t[2] = a3 - a2; t[3] = ns + 10 * ok + 100 * ok2;
+    }
+    __syncthreads();
+    // 64 lanes, one hypothesis each, serial solutions (old layout)
+    load(lane);
+    long long b0 = wall_clock64();
+    int ok = vg::p3p_solve4(k, o, im, R, T);
+    __syncthreads();
+    long long b1 = wall_clock64();
+    // 16 hypotheses x 4 solution lanes (new layout)
+    load(lane >> 2);
+    int ok2 = vg::p3p_solution(k, o, im, lane & 3, R, T, &e);
+    __syncthreads();
+    long long b2 = wall_clock64();
+    if (lane == 0) { t[4] = b1 - b0; t[5] = b2 - b1; t[6] = ok + ok2; }
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-int main()
+int main(int argc, char** argv)
 {
+    const int outl_pct = argc > 1 ? atoi(argv[1]) : 10;
     const int n = 700;
     double K[9] = {718.856, 0, 607.1928, 0, 718.856, 185.2157, 0, 0, 1};
     std::vector<double> pws(3 * n), us(2 * n);
@@ -60,7 +103,7 @@ int main()
         double X = U(-10, 10), Y = U(-2, 2), Z = U(5, 60);
         pws[3 * i] = X; pws[3 * i + 1] = Y; pws[3 * i + 2] = Z;
         double u = K[0] * (X + 0.1) / (Z + 1.0) + K[2], v = K[4] * Y / (Z + 1.0) + K[5];
-        if (i % 10 == 0) { u += U(20, 60); v -= U(20, 60); }
+        if (i % 100 < outl_pct) { u += U(20, 60); v -= U(20, 60); }
         us[2 * i] = u; us[2 * i + 1] = v;
         objf[3 * i] = X; objf[3 * i + 1] = Y; objf[3 * i + 2] = Z;
         imgf[2 * i] = u; imgf[2 * i + 1] = v;
@@ -92,6 +135,12 @@ int main()
         hipLaunchKernelGGL(k_t_epnp, dim3(1), dim3(256), 0, 0, dK, dp, du, dal, dpc, n, dout, dt);
         CK(hipDeviceSynchronize()); CK(hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost));
         printf("epnp_block n=%d: %lld cycles\n", n, t);
+    }
+    for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(k_t_p3p_parts, dim3(1), dim3(64), 0, 0, dK, dp, du, n, dt);
+        long long tt[8]; CK(hipDeviceSynchronize()); CK(hipMemcpy(tt, dt, 64, hipMemcpyDeviceToHost));
+        printf("p3p parts (us): lengths %.2f, solution0 %.2f, solve4 %.2f (flags %lld) | wave: 64 hyps serial-solutions %.2f, 16x4 lanes %.2f\n",
+               tt[0] / 100.0, tt[1] / 100.0, tt[2] / 100.0, tt[3], tt[4] / 100.0, tt[5] / 100.0);
     }
     // whole RANSAC for one chain
     float *dobj, *dimg; int32_t *dcnt, *dsucc, *dninl; uint8_t* dmask; double *dwork, *drv, *dtv; int32_t* diw;
