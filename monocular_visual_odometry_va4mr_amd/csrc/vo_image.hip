@@ -391,6 +391,27 @@ __global__ void __launch_bounds__(64) k_lk(LKParams P, int level, int B, int nb)
     }
 }
 
+#ifdef VO_LK_PROF
+// per level, per block (first 1024): start, end (wall clock, 100 MHz), iterations, J stagings
+__device__ long long g_lkprof[VO_MAX_LEVELS][1024][4];
+#define LKPROF_SET(k, v) do { if (lane == 0 && blockIdx.x < 1024) g_lkprof[level][blockIdx.x][k] = (v); } while (0)
+#define LKPROF_ADD(k, v) do { if (lane == 0 && blockIdx.x < 1024) g_lkprof[level][blockIdx.x][k] += (v); } while (0)
+#else
+#define LKPROF_SET(k, v) do { } while (0)
+#define LKPROF_ADD(k, v) do { } while (0)
+#endif
+
+#ifdef VO_LK_CHECK
+// diagnostics build: bounds-check every global load of k_lk_w against its chain's buffer;
+// a bad address is reported and not dereferenced
+#define LKCHK(ptr, base, bytes, what) \
+    (((const char*)(ptr) >= (const char*)(base) && (const char*)(ptr) + 4 <= (const char*)(base) + (bytes)) ? true : \
+     (printf("LKCHK %s b=%d p=%d level=%d off=%lld size=%lld\n", what, b, pcur, level, \
+             (long long)((const char*)(ptr) - (const char*)(base)), (long long)(bytes)), false))
+#else
+#define LKCHK(ptr, base, bytes, what) true
+#endif
+
 // ---------------------------------------------------------------------------------------
 // k_lk_w<WW, WH>: the same LK level as k_lk for a compile-time window (the reference uses
 // 15x15 for every dataset, main.py:36,66,96), with all window data staged through LDS by
@@ -403,7 +424,7 @@ __global__ void __launch_bounds__(64) k_lk(LKParams P, int level, int B, int nb)
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
 template <int WW, int WH>
-__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int nb, int xcd)
+__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
 {
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
@@ -414,20 +435,19 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
     __shared__ uint32_t DR[(WH + 1) * DRW];
     const uint8_t* jr8 = (const uint8_t*)JR;
     const uint8_t* ir8 = (const uint8_t*)IR;
-    int b, pb;
+    int b, pb, pcur = -1;
+    const int lane = lane_id();
+    int level = level_lo;
+    LKPROF_SET(0, wall_clock64()); LKPROF_SET(1, 0);
+    for (level = level_hi; level >= level_lo; --level) { LKPROF_SET(2, 0); LKPROF_SET(3, 0); }
+    level = level_lo;
     if (!lk_block(B, nb, b, pb, xcd != 0)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
-    const int lane = lane_id();
     const int n0 = P.n0 ? P.n0[b] : 0;
     int n1 = P.n1 ? P.n1[b] : 0;
     if (n1 <= P.seg1_min) n1 = 0;
     const int ntot = n0 + n1;
     const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
-    const int cols = P.lw[level], rows = P.lh[level], pitch = P.lpitch[level];
-    const uint8_t* I = P.prev + b * P.pstride + P.loff[level];
-    const int16_t* DI = P.der + b * P.dstride + 2 * P.loff[level];
-    const uint8_t* J = P.next + b * P.pstride + P.loff[level];
-    const float sc = (float)(1. / (1 << level));
     int wyv[MAXJ], wxv[MAXJ];
     bool live[MAXJ];
 #pragma unroll
@@ -438,6 +458,10 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
         wxv[j] = live[j] ? k - (k / WW) * WW : 0;
     }
     int tx0 = 0, ty0 = 0, jsh = 0;
+    int cols = 0, rows = 0, pitch = 0;
+    const uint8_t* I = nullptr;
+    const int16_t* DI = nullptr;
+    const uint8_t* J = nullptr;
     // (re)stage the J tile so that it covers the window at (inx, iny)
     auto stage_j = [&](int inx, int iny) {
         tx0 = max(inx - LK_M, -VO_BORDER);
@@ -445,10 +469,12 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
         const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
         jsh = gx0 & 3;
         const uint8_t* rowp = J + (int64_t)gy0 * pitch + (gx0 & ~3);
+        LKPROF_ADD(3, 1);
         wave_lds_sync();
         for (int q = lane; q < (TH + 1) * JRW; q += 64) {
             const int r = q / JRW, c = q - r * JRW;
-            JR[q] = *(const uint32_t*)(rowp + (int64_t)r * pitch + 4 * c);
+            const uint8_t* ja = rowp + (int64_t)r * pitch + 4 * c;
+            JR[q] = LKCHK(ja, P.next + (int64_t)b * P.pstride, P.pstride, "J") ? *(const uint32_t*)ja : 0u;
         }
         wave_lds_sync();
         for (int q = lane; q < TH * TW; q += 64) {
@@ -461,18 +487,36 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
     for (int p = pb + 0; p < ntot; p += nb) {
         const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
         const int64_t oidx = (int64_t)b * P.ocap + p;
+        pcur = p;
+#ifdef VO_LK_CHECK
+        if ((p < n0 && p >= P.cap0) || (p >= n0 && p - n0 >= P.cap1) || p >= P.ocap) {
+            if (lane == 0) printf("LKCHK src b=%d p=%d n0=%d n1=%d\n", b, p, n0, n1);
+            continue;
+        }
+#else
+        (void)pcur;
+#endif
         // per-point values are wave-uniform: keep them (and the addresses built from them)
         // in scalar registers
         const float ptx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(src[0])));
         const float pty = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(src[1])));
         int status = 1;
         float errv = 0.f;
+        float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
+        for (level = level_hi; level >= level_lo; --level) {
+        cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level];
+        I = P.prev + b * P.pstride + P.loff[level];
+        DI = P.der + b * P.dstride + 2 * P.loff[level];
+        J = P.next + b * P.pstride + P.loff[level];
+        const float sc = (float)(1. / (1 << level));
         float px = ptx * sc, py = pty * sc;
-        float ox, oy;   // nextPts[ptidx]
         if (level == P.L) { ox = px; oy = py; }
-        else {
+        else if (level == level_hi) {
             ox = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.out[2 * oidx]))) * 2.f;
             oy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(P.out[2 * oidx + 1]))) * 2.f;
+        } else {                // fused levels: the previous level's estimate, still in registers
+            ox *= 2.f;
+            oy *= 2.f;
         }
         px -= hx;
         py -= hy;
@@ -492,11 +536,13 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
                 wave_lds_sync();
                 for (int q = lane; q < (WH + 1) * IRW; q += 64) {
                     const int r = q / IRW, c = q - r * IRW;
-                    IR[q] = *(const uint32_t*)(irow + (int64_t)r * pitch + 4 * c);
+                    const uint8_t* ia = irow + (int64_t)r * pitch + 4 * c;
+                    IR[q] = LKCHK(ia, P.prev + (int64_t)b * P.pstride, P.pstride, "I") ? *(const uint32_t*)ia : 0u;
                 }
                 for (int q = lane; q < (WH + 1) * DRW; q += 64) {
                     const int r = q / DRW, c = q - r * DRW;
-                    DR[q] = drow[(int64_t)r * pitch + c];
+                    const uint32_t* da = drow + (int64_t)r * pitch + c;
+                    DR[q] = LKCHK(da, P.der + (int64_t)b * P.dstride, 2 * P.dstride, "D") ? *da : 0u;
                 }
                 wave_lds_sync();
                 float a = px - ipx, bb = py - ipy;
@@ -589,6 +635,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
                     }
                     pdx = ddx;
                     pdy = ddy;
+                    LKPROF_ADD(2, 1);
                 }
                 if (status && level == 0) {
                     const float fx = ox - hx, fy = oy - hy;
@@ -621,15 +668,18 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level, int B, int n
                 }
             }
         } while (false);
+        }   // levels
         if (lane == 0) {
             P.out[2 * oidx] = ox;
             P.out[2 * oidx + 1] = oy;
-            if (level == 0) {
+            if (level_lo == 0) {
                 P.st[oidx] = (uint8_t)status;
                 if (P.err) P.err[oidx] = errv;
             }
         }
     }
+    level = level_lo;
+    LKPROF_SET(1, wall_clock64());
 }
 
 // ---------------------------------------------------- tracking compaction (:282-290)
@@ -1334,8 +1384,16 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     const bool staged15 = P.win_w == 15 && P.win_h == 15 && P.pstride >= pyr_end + 64;
     const size_t lds = 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
     if (lds > 60 * 1024) return VO_EARG;
+    // Fused levels (one launch, each wave carries its point from the coarsest level to level
+    // 0 in registers) unless VO_LK_FUSED=0: a level's launch lasts as long as its slowest
+    // point (up to max_count iterations), so separate launches pay that tail once per level.
+    static const int fused_env = [] { const char* e = getenv("VO_LK_FUSED"); return e ? atoi(e) : 1; }();
+    if (staged15 && fused_env) {
+        hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
+        return hip_ok() ? VO_OK : VO_EHIP;
+    }
     for (int level = P.L; level >= 0; --level) {
-        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, B, nb, xcd_env);
+        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
         else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
         else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }
@@ -1370,6 +1428,13 @@ extern "C" int vo_lk_points(const vo_dims* d, const vo_opts* o, const vo_state* 
     P.out = out_pts; P.st = out_status; P.err = out_err; P.ocap = cap;
     return launch_lk(P, d->B, VO_STREAM(stream));
 }
+
+#ifdef VO_LK_PROF
+extern "C" int vo_lk_prof_read(long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lkprof), sizeof g_lkprof) == hipSuccess ? VO_OK : VO_EHIP;
+}
+#endif
 
 extern "C" int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream)
 {

@@ -482,19 +482,20 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
         const int CH = it0 == 0 ? VO_PNP_CH1 : HYP;
         PNPPROF(1);
         if (tid == 0) {
+            // getSubset (oracle get_subset): four distinct draws, kept in registers so the
+            // duplicate checks do not wait on LDS
+            const uint32_t un = (uint32_t)n;
             for (int h = 0; h < CH; ++h) {
-                for (int i = 0; i < 4; ++i) {
-                    for (;;) {
-                        int v = (int)(rng_next(rng) % (uint32_t)n);
-                        int j;
-                        for (j = 0; j < i; ++j) if (v == sub[h][j]) break;
-                        sub[h][i] = v;
-                        if (j == i) break;
-                    }
-                }
+                const int s0 = (int)(rng_next(rng) % un);
+                int s1, s2, s3;
+                do { s1 = (int)(rng_next(rng) % un); } while (s1 == s0);
+                do { s2 = (int)(rng_next(rng) % un); } while (s2 == s0 || s2 == s1);
+                do { s3 = (int)(rng_next(rng) % un); } while (s3 == s0 || s3 == s1 || s3 == s2);
+                sub[h][0] = s0; sub[h][1] = s1; sub[h][2] = s2; sub[h][3] = s3;
             }
         }
         __syncthreads();
+        PNPPROF(6);
         {
             // four lanes per hypothesis, one P3P solution each (p3p_solution); the lanes then
             // apply p3p_solve4's rule (first solution with a strictly smaller 4th-point error)

@@ -166,8 +166,8 @@ int main(int argc, char** argv)
         printf("k_pnp_ransac 1 chain n=%d: %.3f ms, inliers %d\n", n, ms, ni);
         long long t[32];
         CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_pnpprof), sizeof t));
-        printf("  (us) sample+P3P %.1f, score+update %.1f [last chunk], epnp: mtm %.1f svd12 %.1f betas %.1f R_and_t x3 %.1f | ransac total %.1f compaction %.1f epnp %.1f\n",
-               (t[2] - t[1]) / 100.0, (t[3] - t[2]) / 100.0, (t[10] - t[4]) / 100.0 + 0 * (t[11] - t[10]), (t[11] - t[10]) / 100.0,
+        printf("  (us) sample %.1f P3P %.1f, score+update %.1f [last chunk], epnp: mtm %.1f svd12 %.1f betas %.1f R_and_t x3 %.1f | ransac total %.1f compaction %.1f epnp %.1f\n",
+               (t[6] - t[1]) / 100.0, (t[2] - t[6]) / 100.0, (t[3] - t[2]) / 100.0, (t[10] - t[4]) / 100.0 + 0 * (t[11] - t[10]), (t[11] - t[10]) / 100.0,
                (t[12] - t[11]) / 100.0, (t[13] - t[12]) / 100.0, (t[3] - t[0]) / 100.0, (t[4] - t[3]) / 100.0, (t[5] - t[4]) / 100.0);
     }
     return 0;
