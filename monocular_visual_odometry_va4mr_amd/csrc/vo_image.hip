@@ -392,13 +392,19 @@ __global__ void __launch_bounds__(64) k_lk(LKParams P, int level, int B, int nb)
 }
 
 #ifdef VO_LK_PROF
-// per level, per block (first 1024): start, end (wall clock, 100 MHz), iterations, J stagings
-__device__ long long g_lkprof[VO_MAX_LEVELS][1024][4];
+// per level, per block (first 1024): start, end (wall clock, 100 MHz), iterations, J stagings,
+// then wall-clock ticks spent in: I/dI staging, structure tensor, J staging, iterations
+__device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 #define LKPROF_SET(k, v) do { if (lane == 0 && blockIdx.x < 1024) g_lkprof[level][blockIdx.x][k] = (v); } while (0)
 #define LKPROF_ADD(k, v) do { if (lane == 0 && blockIdx.x < 1024) g_lkprof[level][blockIdx.x][k] += (v); } while (0)
 #else
 #define LKPROF_SET(k, v) do { } while (0)
 #define LKPROF_ADD(k, v) do { } while (0)
+#endif
+#ifdef VO_LK_PROF
+#define LKPROF_T(var) const long long var = wall_clock64()
+#else
+#define LKPROF_T(var) do { } while (0)
 #endif
 
 #ifdef VO_LK_CHECK
@@ -439,7 +445,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     const int lane = lane_id();
     int level = level_lo;
     LKPROF_SET(0, wall_clock64()); LKPROF_SET(1, 0);
-    for (level = level_hi; level >= level_lo; --level) { LKPROF_SET(2, 0); LKPROF_SET(3, 0); }
+    for (level = level_hi; level >= level_lo; --level)
+        for (int k = 2; k < 8; ++k) LKPROF_SET(k, 0);
     level = level_lo;
     if (!lk_block(B, nb, b, pb, xcd != 0)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
@@ -470,6 +477,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
         jsh = gx0 & 3;
         const uint8_t* rowp = J + (int64_t)gy0 * pitch + (gx0 & ~3);
         LKPROF_ADD(3, 1);
+        LKPROF_T(tj0);
         wave_lds_sync();
         for (int q = lane; q < (TH + 1) * JRW; q += 64) {
             const int r = q / JRW, c = q - r * JRW;
@@ -483,6 +491,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
             QT[q] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[4 * JRW] << 16) | ((uint32_t)s[4 * JRW + 1] << 24);
         }
         wave_lds_sync();
+        LKPROF_T(tj1);
+        LKPROF_ADD(6, tj1 - tj0);
     };
     for (int p = pb + 0; p < ntot; p += nb) {
         const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
@@ -529,6 +539,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
             // stage I (u8) and dI (int16 x2) rows under the window
             bool staged = false;
             {
+                LKPROF_T(ti0);
                 const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
                 const int ish = gx & 3;
                 const uint8_t* irow = I + (int64_t)gy * pitch + (gx & ~3);
@@ -545,6 +556,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     DR[q] = LKCHK(da, P.der + (int64_t)b * P.dstride, 2 * P.dstride, "D") ? *da : 0u;
                 }
                 wave_lds_sync();
+                LKPROF_T(ti1);
+                LKPROF_ADD(4, ti1 - ti0);
                 float a = px - ipx, bb = py - ipy;
                 const int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
                 const int iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
@@ -582,6 +595,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 D = 1.f / D;
                 float nx = ox - hx, ny = oy - hy;
                 float pdx = 0.f, pdy = 0.f;
+                LKPROF_T(ta1);
+                LKPROF_ADD(5, ta1 - ti1);
                 for (int it = 0; it < P.max_count; ++it) {
                     const int inx = (int)floorf(nx), iny = (int)floorf(ny);
                     if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
@@ -636,6 +651,10 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     pdx = ddx;
                     pdy = ddy;
                     LKPROF_ADD(2, 1);
+                }
+                {
+                    LKPROF_T(te);
+                    LKPROF_ADD(7, te - ta1);
                 }
                 if (status && level == 0) {
                     const float fx = ox - hx, fy = oy - hy;

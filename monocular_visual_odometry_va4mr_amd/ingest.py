@@ -1,10 +1,16 @@
-"""Frame ingest: dataset PNGs -> pinned host batches -> HBM.
+"""Frame ingest: dataset images -> pinned host batches -> HBM.
 
 The reference reads one frame per step with cv2.imread(path, IMREAD_GRAYSCALE)
-(utils.py:55-81).  Here libvo_ingest.so decodes a whole batch (one frame per chain) on a
-pool of host threads into pinned memory, a Python thread keeps one batch ahead of the
-consumer, and the host->HBM copy runs on its own stream, so decoding and the copy overlap
-the GPU step of the previous batch.
+(utils.py:55-81).  Here libvo_ingest.so decodes a whole batch of PNGs (KITTI, Parking; one
+frame per chain) on a pool of host threads into pinned memory, a Python thread keeps one
+batch ahead of the consumer, and the host->HBM copy runs on its own stream, so decoding and
+the copy overlap the GPU step of the previous batch.
+
+Malaga's JPEGs go through libjpeg (via PIL, which releases the GIL while decoding) on a
+thread pool, asking the decoder for grayscale output the way OpenCV's JPEG reader does for
+IMREAD_GRAYSCALE (out_color_space = JCS_GRAYSCALE: the Y channel, no RGB round trip).
+rocJPEG is not part of this ROCm image, so there is no device JPEG path.  Parity with
+OpenCV's bundled libjpeg-turbo is unpinned (no cv2 here); both use the ISLOW IDCT.
 """
 from __future__ import annotations
 
@@ -52,10 +58,40 @@ def png_info(data: bytes):
     return w.value, h.value, c.value, d.value
 
 
+_PNG_SIG = b"\x89PNG\r\n\x1a\n"
+_JPEG_SIG = b"\xff\xd8\xff"
+
+
+def is_jpeg(path: str) -> bool:
+    with open(path, "rb") as f:
+        return f.read(3) == _JPEG_SIG
+
+
+def jpeg_gray(path: str, out: np.ndarray | None = None) -> np.ndarray:
+    """Y channel of a baseline/progressive JPEG as uint8 [H, W] (libjpeg grayscale output)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        if im.format != "JPEG":
+            raise ValueError(f"{path}: not a JPEG")
+        im.draft("L", im.size)              # decoder-side colour conversion to gray, scale 1/1
+        if im.mode != "L":                  # CMYK / odd layouts: fall back to PIL's conversion
+            im = im.convert("L")
+        arr = np.asarray(im, dtype=np.uint8)
+    if out is None:
+        return arr.copy()
+    if out.shape != arr.shape:
+        raise ValueError(f"{path}: size {arr.shape[::-1]} != expected {out.shape[::-1]}")
+    out[...] = arr
+    return out
+
+
 def imread_gray(path: str) -> np.ndarray:
-    """cv2.imread(path, cv2.IMREAD_GRAYSCALE) for PNG files (utils.py:59,81)."""
+    """cv2.imread(path, cv2.IMREAD_GRAYSCALE) for the datasets' PNG and JPEG files
+    (utils.py:59,70,81)."""
     with open(path, "rb") as f:
         data = f.read()
+    if data[:3] == _JPEG_SIG:
+        return jpeg_gray(path)
     w, h, _, _ = png_info(data)
     out = np.empty((h, w), np.uint8)
     rc = lib().vo_png_decode_gray(data, len(data), out.ctypes.data, w, w, h)
@@ -65,7 +101,7 @@ def imread_gray(path: str) -> np.ndarray:
 
 
 class FrameSource:
-    """Iterate over batches of PNG paths (batches[j][b] = frame of chain b at step j) and yield
+    """Iterate over batches of PNG/JPEG paths (batches[j][b] = frame of chain b at step j) and yield
     uint8 [B, H, W] tensors on `device`, decoded one batch ahead of the consumer."""
 
     def __init__(self, batches, width: int, height: int, device="cuda", threads: int = 8, depth: int = 2):
@@ -80,6 +116,7 @@ class FrameSource:
         for i in range(len(self._bufs)):
             self._free.put(i)
         self._ready = queue.Queue()
+        self._threads = int(threads)
         self._pool = lib().vo_ingest_create(int(threads))
         self._copy_stream = torch.cuda.Stream(self.device) if gpu else None
         self._thread = threading.Thread(target=self._decode_all, daemon=True)
@@ -91,12 +128,43 @@ class FrameSource:
             slot = self._free.get()
             if slot is None:
                 return
-            arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+            jpg = [i for i, p in enumerate(paths) if p.lower().endswith((".jpg", ".jpeg"))]
             st = np.zeros(len(paths), np.int32)
-            rc = L.vo_ingest_png_files(self._pool, arr, len(paths), self._bufs[slot].data_ptr(),
-                                       self.H * self.W, self.W, self.H, st.ctypes.data)
+            rc = 0
+            if len(jpg) < len(paths):
+                png = [i for i in range(len(paths)) if i not in set(jpg)] if jpg else list(range(len(paths)))
+                if len(png) == len(paths):
+                    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+                    rc = L.vo_ingest_png_files(self._pool, arr, len(paths), self._bufs[slot].data_ptr(),
+                                               self.H * self.W, self.W, self.H, st.ctypes.data)
+                else:                       # mixed batch: PNGs one by one through the pool
+                    for i in png:
+                        arr = (C.c_char_p * 1)(os.fsencode(paths[i]))
+                        one = np.zeros(1, np.int32)
+                        r = L.vo_ingest_png_files(self._pool, arr, 1, self._bufs[slot][i].data_ptr(),
+                                                  self.H * self.W, self.W, self.H, one.ctypes.data)
+                        st[i] = one[0]
+                        rc = rc or r
+            if jpg:
+                host = self._bufs[slot].numpy()
+
+                def dec(i):
+                    try:
+                        jpeg_gray(paths[i], host[i])
+                        return 0
+                    except Exception:       # reported below like a PNG decode failure
+                        return -4
+                for i, r in zip(jpg, self._jpeg_pool().map(dec, jpg)):
+                    st[i] = r
+                    rc = rc or r
             self._ready.put((j, slot, rc, st))
         self._ready.put(None)
+
+    def _jpeg_pool(self):
+        if getattr(self, "_jpool", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._jpool = ThreadPoolExecutor(max_workers=self._threads)
+        return self._jpool
 
     def __len__(self):
         return len(self.batches)
@@ -133,6 +201,9 @@ class FrameSource:
     def close(self):
         self._free.put(None)
         self._thread.join(timeout=10)
+        if getattr(self, "_jpool", None) is not None:
+            self._jpool.shutdown(wait=True)
+            self._jpool = None
         if self._pool:
             lib().vo_ingest_destroy(self._pool)
             self._pool = None

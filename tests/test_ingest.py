@@ -91,3 +91,39 @@ def test_ingest_header_symbols_exported():
     import re
     declared = set(re.findall(r"\b(vo_[a-z0-9_]+)\s*\(", hdr))
     assert declared and declared <= defined, declared - defined
+
+
+def test_jpeg_gray_matches_decoder_luma(tmp_path, frames):
+    """Malaga JPEGs: grayscale straight from the decoder (the Y plane), like OpenCV's
+    IMREAD_GRAYSCALE JPEG path; a gray JPEG decodes to PIL's own result exactly."""
+    from monocular_visual_odometry_va4mr_amd import ingest
+    p = tmp_path / "g.jpg"
+    PIL.fromarray(frames[0], mode="L").save(p, quality=95)
+    g = ingest.imread_gray(str(p))
+    assert g.dtype == np.uint8 and g.shape == frames[0].shape
+    assert np.array_equal(g, np.asarray(PIL.open(p)))
+    assert np.abs(g.astype(int) - frames[0]).mean() < 3.0            # lossy but close
+    rgb = np.stack([frames[0], frames[1], frames[2]], -1)
+    p = tmp_path / "c.jpg"
+    PIL.fromarray(rgb, mode="RGB").save(p, quality=95)
+    y = ingest.imread_gray(str(p))
+    ycc = np.asarray(PIL.open(p).convert("YCbCr"))[..., 0]            # luma via RGB round trip
+    assert y.shape == rgb.shape[:2] and np.abs(y.astype(int) - ycc).max() <= 3
+    assert ingest.is_jpeg(str(p))
+
+
+def test_frame_source_jpeg_and_mixed_batches(tmp_path, frames):
+    from monocular_visual_odometry_va4mr_amd import ingest
+    paths = []
+    for i, f in enumerate(frames):
+        p = tmp_path / (f"f{i}.jpg" if i % 2 == 0 else f"f{i}.png")
+        PIL.fromarray(f, mode="L").save(p, **({"quality": 97} if i % 2 == 0 else {}))
+        paths.append(str(p))
+    h, w = frames[0].shape
+    src = ingest.FrameSource([paths[:2], paths[2:3] + paths[:1]], w, h, device="cpu", threads=2)
+    out = [b.clone() for b in src]
+    src.close()
+    assert len(out) == 2 and tuple(out[0].shape) == (2, h, w)
+    assert np.array_equal(out[0][1].numpy(), frames[1])               # PNG: exact
+    assert np.array_equal(out[0][0].numpy(), ingest.imread_gray(paths[0]))
+    assert np.array_equal(out[1][0].numpy(), ingest.imread_gray(paths[2]))

@@ -33,7 +33,7 @@ vo.initialization(fr[boot[0]], fr[boot[1]])
 for i in range(boot[1] + 1, n):
     vo.continuous_operation(fr[i])
 torch.cuda.synchronize()
-buf = np.zeros((L.VO_MAX_LEVELS, 1024, 4), np.int64)
+buf = np.zeros((L.VO_MAX_LEVELS, 1024, 8), np.int64)
 lib = L.lib()
 lib.vo_lk_prof_read.restype = C.c_int
 assert lib.vo_lk_prof_read(C.c_void_p(buf.ctypes.data)) == 0
@@ -44,9 +44,11 @@ t0 = buf[:, :, 0][buf[:, :, 0] > 0].min()
 for lv in range(eng.dims.nlev - 1, -1, -1):
     b = buf[lv]
     used = b[:, 1] > 0
+    ph = b[:npts, 4:8].mean(0) / 100.0
+    phases = f"phases us/point: I-stage {ph[0]:5.2f} tensor {ph[1]:5.2f} J-stage {ph[2]:5.2f} iterations(+restage) {ph[3]:5.2f}"
     if not used.any():      # fused launch: only level 0 holds the block times
         it = b[:npts, 2]
-        print(f"level {lv}: iters mean {it.mean():5.2f} max {it.max():3d}")
+        print(f"level {lv}: iters mean {it.mean():5.2f} max {it.max():3d} | {phases}")
         continue
     st, en = b[used, 0], b[used, 1]
     dur = (en - st) / 100.0
@@ -56,3 +58,4 @@ for lv in range(eng.dims.nlev - 1, -1, -1):
           f"| block us mean {dur.mean():5.2f} p50 {np.median(dur):5.2f} p99 {np.percentile(dur, 99):6.2f} max {dur.max():6.2f} "
           f"| iters mean {it.mean():5.2f} max {it.max():3d} (slowest block: {it[k]} iters, {sg[k]} stagings) "
           f"| start spread {(st.max() - st.min()) / 100.0:5.1f} us")
+    print("    " + phases)
