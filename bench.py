@@ -100,10 +100,11 @@ def klt_bytes(eng, n_pts):
 
 
 def pyr_bytes(eng):
-    """u8 frame read + pyramid write (levels >= 1) + int16x2 derivative write, per chain."""
+    """vo_pyr_build: u8 frame read + every pyramid level written (u8, interior pixels) + the
+    int16x2 Scharr derivatives of every level written, per chain."""
     d = eng.dims
     spx = sum(d.lvl_w[i] * d.lvl_h[i] for i in range(d.nlev))
-    return float(eng.B * (2 * eng.W * eng.H + (spx - eng.W * eng.H) + 4 * spx))
+    return float(eng.B * (eng.W * eng.H + spx + 4 * spx))
 
 
 def gftt_bytes(eng, n_corners):
@@ -279,8 +280,7 @@ def main():
     bytes_by = {
         "track": klt_bytes(eng, npts),
         "gftt": gftt_bytes(eng, ncor),
-        "pyr_build": float(eng.B * (eng.W * eng.H + sum(eng.dims.lvl_w[i] * eng.dims.lvl_h[i]
-                                                           for i in range(1, eng.dims.nlev)))),
+        "pyr_build": pyr_bytes(eng),
     }
     # dominant HBM-class stage (pyramid/KLT/detection are judged by bytes)
     dom = max(bytes_by, key=lambda n: st_ms[names.index(n)])

@@ -83,7 +83,7 @@ typedef struct vo_opts {
 /* Device state of B chains; every pointer is [B][...] contiguous per chain. */
 typedef struct vo_state {
     uint8_t* pyr[2];              /* ping-pong image pyramids  [B][pyr_stride]          */
-    int16_t* der;                 /* Scharr of the previous frame [B][der_stride]       */
+    int16_t* der[2];              /* Scharr of pyr[0] / pyr[1]    [B][der_stride]       */
     float* lm_X;                  /* matched_landmarks  [B][ncap][3]                     */
     float* lm_kp;                 /* matched_keypoints  [B][ncap][2]                     */
     int32_t* nL;                  /* [B]                                                 */
@@ -124,11 +124,14 @@ int vo_device_arch(char* buf, int len);          /* gcnArchName of the current d
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 
-/* Build the pyramid of the new frames into state->pyr[cur] (part of cv2.calcOpticalFlowPyrLK,
- * :281,287).  frames: [B][H][W] u8, frame_stride bytes between chains. */
+/* Build the pyramid of the new frames into state->pyr[cur] and its Scharr derivatives into
+ * state->der[cur] (buildOpticalFlowPyramid + calcSharrDeriv inside cv2.calcOpticalFlowPyrLK,
+ * :281,287), one fused pass per level.  frames: [B][H][W] u8, frame_stride bytes between
+ * chains.  The derivative buffers' zero border is never written (allocate them zeroed). */
 int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
                  int64_t frame_stride, vo_stream_t stream);
-/* Scharr derivatives of pyramid `which` into state->der (calcSharrDeriv). */
+/* Scharr derivatives of pyramid `which` into state->der[which] (calcSharrDeriv), border
+ * included; vo_pyr_build already produces them, this recomputes them alone. */
 int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t stream);
 
 /* feature_tracking (:271-290): LK of landmarks and (if P > 1) candidates from pyr[prev]

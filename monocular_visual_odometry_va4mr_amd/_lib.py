@@ -70,7 +70,7 @@ class VoOpts(C.Structure):
 
 
 _STATE_FIELDS = [
-    "pyr0", "pyr1", "der", "lm_X", "lm_kp", "nL", "c_kp", "c_first", "c_tau", "nC",
+    "pyr0", "pyr1", "der0", "der1", "lm_X", "lm_kp", "nL", "c_kp", "c_first", "c_tau", "nC",
     "pose_R", "pose_t", "nF", "num_pts", "outl_kp", "inl_kp", "nOutl", "nInl", "status",
     "trk_pts", "trk_st", "trk_err", "eig", "eig_max", "gf_keys", "gf_n", "corners", "nCorners",
     "pnp_rt", "pnp_ok", "pnp_ninl", "pnp_mask", "work", "iwork",

@@ -21,77 +21,156 @@ namespace {
 // vector (16, 4 or 16 bytes).  Bytes between the padded width and the pitch may be written
 // with don't-care values.
 
-// level 0 (frame copy + border): a wave writes 1024 output bytes of one row, 16 per lane; the
-// (unaligned) source row segment is first read into LDS with coalesced loads
-__global__ void __launch_bounds__(256) k_ingest(const uint8_t* __restrict__ frames, int64_t fstride,
-                                                uint8_t* __restrict__ pyr, int64_t pstride, int W, int H,
-                                                int pitch, int64_t off, int ph)
-{
-    __shared__ uint8_t segs[4][1024 + 4];
-    uint8_t* seg = segs[wave_id()];
-    const int b = blockIdx.z;
-    const int x0 = blockIdx.x * 1024;                 // first output column of this wave
-    const int py = blockIdx.y * 4 + wave_id();
-    const int pw = W + 2 * VO_BORDER;
-    if (py >= ph) return;
-    const uint8_t* srow = frames + b * fstride + (int64_t)refl101(py - VO_BORDER, H) * W;
-    // interior source columns covered here: [x0 - B, x0 + 1024 - B) clipped to [0, W)
-    const int s0 = max(x0 - VO_BORDER, 0), s1 = min(x0 + 1024 - VO_BORDER, W);
-    const int lane = lane_id();
-    for (int i = lane; i < s1 - s0; i += 64) seg[i] = srow[s0 + i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int px0 = x0 + lane * 16;
-    if (px0 >= pw) return;
-    uint32_t w4[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int px = px0 + 4 * q + k;
-            uint32_t byte = 0;
-            if (px < pw) {
-                const int sx = refl101(px - VO_BORDER, W);
-                byte = (sx >= s0 && sx < s1) ? seg[sx - s0] : srow[sx];   // borders: reflected
-            }
-            v |= byte << (8 * k);
-        }
-        w4[q] = v;
-    }
-    *(uint4*)(pyr + b * pstride + off + (int64_t)py * pitch + px0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-}
+// One pyramid level and its Scharr derivatives in one pass (buildOpticalFlowPyramid +
+// calcSharrDeriv semantics).  A 256-thread block owns a PT_W x PT_H tile of
+// the padded level: it materialises the level's values (with the reflect-101 border and a
+// 1-pixel halo) in LDS, writes the tile to the pyramid with dword stores, and computes the
+// int16 (dx, dy) Scharr of the tile's interior pixels from the same LDS tile.
+//  * level 0: the values are frame bytes at reflect-101 coordinates;
+//  * level l >= 1: cv::pyrDown of level l-1 ([1 4 6 4 1]^2 / 256).  The source rectangle
+//    under the tile is staged with aligned dword loads, filtered horizontally once per
+//    staged row into LDS, then vertically per output pixel (exact integers; the order of
+//    the two passes does not change the result).
+// The derivative image's zero border is never written: the derivative buffers are
+// zero-initialised and only interior pixels are stored (zeros fill partial vectors).
+#define PT_W 128
+#define PT_H 16
+#define PV_W (PT_W + 8)                     // tile cols px0-4 .. px0+PT_W+3
+#define PV_H (PT_H + 2)                     // tile rows py0-1 .. py0+PT_H
+#define PS_H (2 * PV_H + 3)                 // staged source rows (level >= 1)
+#define PS_W ((2 * PV_W + 3 + 8 + 3) / 4 * 4)  // staged source cols incl. dword alignment slack
 
-// pyrDown (5x5 [1 4 6 4 1]^2 / 256, cv::pyrDown) into the next level incl. border: 4 pixels
-// per lane; source reads stay inside the source's reflect-101 border (|offset| <= 2)
-__global__ void __launch_bounds__(256) k_pyrdown(uint8_t* __restrict__ pyr, int64_t pstride, int sw, int spitch,
-                                                 int64_t soff, int dw, int dh, int dpitch, int64_t doff)
+struct PyrLevelArgs {
+    const uint8_t* src;     // level 0: frames [B][H][W]; else the pyramid (level l-1 inside)
+    int64_t sstride;        // per chain: frame bytes or pyramid stride
+    int sw, sh, spitch;     // source level l-1 (level >= 1)
+    int64_t soff;
+    uint8_t* pyr;           // destination pyramid (level l)
+    int64_t pstride;
+    int16_t* der;           // destination derivatives (level l), may be null
+    int64_t dstride;
+    int w, h, pitch;
+    int64_t off;
+    int level;
+};
+
+__global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
 {
+    __shared__ uint32_t PVw[PV_H * PV_W / 4];
+    __shared__ uint32_t SRw[PS_H * PS_W / 4];
+    __shared__ uint16_t HS[PS_H * PV_W];
+    __shared__ int yk[PV_H], xc[PV_W];
+    __shared__ int mm[4];
+    uint8_t* PV = (uint8_t*)PVw;
+    const uint8_t* SR = (const uint8_t*)SRw;
+    const int tid = threadIdx.x;
     const int b = blockIdx.z;
-    const int px0 = (blockIdx.x * 64 + lane_id()) * 4;
-    const int py = blockIdx.y * 4 + wave_id();
-    const int pw = dw + 2 * VO_BORDER;
-    if (px0 >= pw || py >= dh + 2 * VO_BORDER) return;
-    const int iy = refl101(py - VO_BORDER, dh);
-    const uint8_t* src = pyr + b * pstride + soff + (int64_t)(2 * iy - 2 + VO_BORDER) * spitch + VO_BORDER - 2;
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int px = px0 + k;
-        const int ix = refl101(min(px, pw - 1) - VO_BORDER, dw);
-        const uint8_t* col = src + 2 * ix;
-        int acc = 0;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const uint8_t* row = col + (int64_t)i * spitch;
-            const int r = row[0] + 4 * row[1] + 6 * row[2] + 4 * row[3] + row[4];
-            acc += (i == 0 || i == 4 ? 1 : (i == 2 ? 6 : 4)) * r;
-        }
-        v |= (uint32_t)((acc + 128) >> 8) << (8 * k);
+    const int px0 = blockIdx.x * PT_W, py0 = blockIdx.y * PT_H;
+    const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
+    // level coordinates of the tile's rows / cols (-1: outside the padded level)
+    if (tid < 4) mm[tid] = (tid & 1) ? -1 : 0x7fffffff;
+    __syncthreads();
+    if (tid < PV_H) {
+        const int py = py0 - 1 + tid;
+        const int y = (py >= 0 && py < ph) ? refl101(py - VO_BORDER, A.h) : -1;
+        yk[tid] = y;
+        if (y >= 0) { atomicMin(&mm[0], y); atomicMax(&mm[1], y); }
     }
-    (void)sw;
-    *(uint32_t*)(pyr + b * pstride + doff + (int64_t)py * dpitch + px0) = v;
+    if (tid < PV_W) {
+        const int px = px0 - 4 + tid;
+        const int x = (px >= 0 && px < pw) ? refl101(px - VO_BORDER, A.w) : -1;
+        xc[tid] = x;
+        if (x >= 0) { atomicMin(&mm[2], x); atomicMax(&mm[3], x); }
+    }
+    __syncthreads();
+    if (A.level == 0) {
+        const uint8_t* fr = A.src + (int64_t)b * A.sstride;
+        for (int e = tid; e < PV_H * PV_W; e += 256) {
+            const int k = e / PV_W, c = e - k * PV_W;
+            const int y = yk[k], x = xc[c];
+            PV[e] = (y >= 0 && x >= 0) ? fr[(int64_t)y * A.w + x] : 0;
+        }
+    } else {
+        // source rectangle (level l-1 coordinates) under the tile
+        const int sy0 = 2 * mm[0] - 2, sy1 = 2 * mm[1] + 2;
+        const int sx0 = 2 * mm[2] - 2, sx1 = 2 * mm[3] + 2;
+        const int nsr = sy1 - sy0 + 1;
+        const int gx0 = sx0 + VO_BORDER;                 // padded source column of sx0
+        const int ax0 = gx0 & ~3, sh = gx0 - ax0;
+        const int nwd = (sx1 + VO_BORDER - ax0) / 4 + 1; // dwords per staged row
+        const uint8_t* sbase = A.src + (int64_t)b * A.sstride + A.soff + ax0;
+        for (int e = tid; e < nsr * nwd; e += 256) {
+            const int r = e / nwd, c = e - r * nwd;
+            SRw[r * (PS_W / 4) + c] =
+                *(const uint32_t*)(sbase + (int64_t)(sy0 + r + VO_BORDER) * A.spitch + 4 * c);
+        }
+        __syncthreads();
+        // horizontal [1 4 6 4 1] at the tile's columns, every staged row
+        for (int e = tid; e < nsr * PV_W; e += 256) {
+            const int r = e / PV_W, c = e - r * PV_W;
+            const int x = xc[c];
+            uint16_t v = 0;
+            if (x >= 0) {
+                const uint8_t* q = SR + r * PS_W + sh + (2 * x - 2 - sx0);
+                v = (uint16_t)(q[0] + 4 * q[1] + 6 * q[2] + 4 * q[3] + q[4]);
+            }
+            HS[r * PV_W + c] = v;
+        }
+        __syncthreads();
+        for (int e = tid; e < PV_H * PV_W; e += 256) {
+            const int k = e / PV_W, c = e - k * PV_W;
+            const int y = yk[k];
+            uint8_t v = 0;
+            if (y >= 0 && xc[c] >= 0) {
+                const uint16_t* q = HS + (2 * y - 2 - sy0) * PV_W + c;
+                const int acc = q[0] + 4 * q[PV_W] + 6 * q[2 * PV_W] + 4 * q[3 * PV_W] + q[4 * PV_W];
+                v = (uint8_t)((acc + 128) >> 8);
+            }
+            PV[e] = v;
+        }
+    }
+    __syncthreads();
+    // 4 pixels x 2 rows per thread: pyramid dword stores, then the Scharr of interior pixels
+    const int tc = tid & 31, tr = tid >> 5;
+    const int px = px0 + 4 * tc;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int k = 1 + 2 * tr + rr;
+        const int py = py0 + 2 * tr + rr;
+        if (py >= ph || px >= A.pitch) continue;
+        const uint32_t* rowc = PVw + (k * PV_W) / 4 + 1 + tc;      // cols px..px+3
+        *(uint32_t*)(A.pyr + (int64_t)b * A.pstride + A.off + (int64_t)py * A.pitch + px) = rowc[0];
+        const int y = py - VO_BORDER, x0 = px - VO_BORDER;
+        if (!A.der || y < 0 || y >= A.h || x0 + 3 < 0 || x0 >= A.w) continue;
+        // rows k-1, k, k+1; bytes: col px-1 = byte 3 of dword [-1], px..px+3 = dword [0],
+        // px+4 = byte 0 of dword [1]
+        uint32_t o[4];
+        const uint32_t* ru = rowc - PV_W / 4;
+        const uint32_t* rl = rowc + PV_W / 4;
+        const uint64_t U = ((uint64_t)ru[0] << 8) | (ru[-1] >> 24), L = ((uint64_t)rl[0] << 8) | (rl[-1] >> 24),
+                       Cc = ((uint64_t)rowc[0] << 8) | (rowc[-1] >> 24);
+        const uint64_t U5 = U | ((uint64_t)(ru[1] & 0xff) << 40), L5 = L | ((uint64_t)(rl[1] & 0xff) << 40),
+                       C5 = Cc | ((uint64_t)(rowc[1] & 0xff) << 40);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int dx = 0, dy = 0;
+            const int x = x0 + i;
+            if (x >= 0 && x < A.w) {
+                const int ul = (int)((U5 >> (8 * i)) & 0xff), uc = (int)((U5 >> (8 * i + 8)) & 0xff),
+                          ur = (int)((U5 >> (8 * i + 16)) & 0xff);
+                const int ll = (int)((L5 >> (8 * i)) & 0xff), lc = (int)((L5 >> (8 * i + 8)) & 0xff),
+                          lr = (int)((L5 >> (8 * i + 16)) & 0xff);
+                const int cl = (int)((C5 >> (8 * i)) & 0xff), cr = (int)((C5 >> (8 * i + 16)) & 0xff);
+                const int t0l = (ul + ll) * 3 + cl * 10;
+                const int t0r = (ur + lr) * 3 + cr * 10;
+                dx = t0r - t0l;
+                dy = ((lr - ur) + (ll - ul)) * 3 + (lc - uc) * 10;
+            }
+            o[i] = (uint32_t)(uint16_t)(int16_t)dx | ((uint32_t)(uint16_t)(int16_t)dy << 16);
+        }
+        *(uint4*)(A.der + (int64_t)b * A.dstride + 2 * (A.off + (int64_t)py * A.pitch + px)) =
+            make_uint4(o[0], o[1], o[2], o[3]);
+    }
 }
 
 // Scharr (calcSharrDeriv) of one level: int16 (dx, dy) per pixel, zero outside the image
@@ -892,6 +971,133 @@ __global__ void __launch_bounds__(256) k_eignms(EigParams P)
         }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_eig3: the fused min-eigenvalue + 3x3 local-maximum pass of k_eignms, specialised to the
+// reference's configuration (blockSize 3, useHarrisDetector False; main.py:31-33,61-63,91-93)
+// as a row-streaming kernel.  One wave owns an E3_OUT-column x E3_TH-row tile; lane = image
+// column (3 halo lanes each side) and the wave slides down the rows keeping every
+// intermediate in registers: the Sobel row terms of the last two image rows, the box row
+// sums of the last two gradient rows, the last two eigen rows.  Horizontal neighbours come
+// from the adjacent lanes through DPP wave shifts.  Integers, the double expression of
+// lambda_min, the reflect-101 handling and the emitted key set are those of k_eignms (the
+// parity tests compare corner lists and eigen maps bit for bit).  Keys are gathered in an
+// LDS buffer and appended with one atomic per E3_CAP-sized batch.
+#define E3_OUT 58
+#define E3_TH 64
+#define E3_CAP 512
+
+VO_DEV int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }   // lane i <- i-1
+VO_DEV int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false); }  // lane i <- i+1
+
+__global__ void __launch_bounds__(64) k_eig3(EigParams P)
+{
+    __shared__ uint64_t kbuf[E3_CAP];
+    const int tiles = P.tiles_x * P.tiles_y;
+    const int item = xcd_item(blockIdx.x, P.B * tiles);
+    if (item >= P.B * tiles) return;
+    const int b = item / tiles, t = item - b * tiles;
+    if (P.chain_status && P.chain_status[b] != 0) return;
+    const int ty = t / P.tiles_x, tx = t - ty * P.tiles_x;
+    const int x0 = tx * E3_OUT, y0 = ty * E3_TH;
+    const int W = P.W, H = P.H;
+    const int lane = lane_id();
+    const int c = x0 - 3 + lane;                         // image column of this lane
+    const int cl = min(c, W + 2);                        // loads stay inside the padded row
+    const uint8_t* colp = P.pyr + (int64_t)b * P.pstride + P.off + (int64_t)VO_BORDER * P.pitch + VO_BORDER + cl;
+    const int g0 = max(y0 - 2, 0), g1 = min(y0 + E3_TH + 1, H - 1);   // gradient / box rows
+    const int e0 = max(y0 - 1, 0);                                     // first eigen row
+    const int o0 = max(y0, 1), o1 = min(y0 + E3_TH, H - 1);            // NMS rows [o0, o1)
+    const int m1 = min(y0 + E3_TH, H);                                 // own rows [y0, m1)
+    const bool own = lane >= 3 && lane < 3 + E3_OUT && c < W;
+    const bool nms_col = own && c >= 1 && c < W - 1;
+    const bool hedge = x0 == 0 || x0 + E3_OUT + 3 > W - 1;             // tile reaches column 0 or W-1
+    const double s = 1.0 / ((double)(1 << 2) * 3 * 255.0);
+    const double sc = s * s * 0.5;
+    uint32_t kmax = 0;
+    int nbuf = 0;
+    uint64_t* out = P.keys ? P.keys + (int64_t)b * P.ccap : nullptr;
+    auto flush = [&]() {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&P.nkeys[b], nbuf);
+        base = __builtin_amdgcn_readfirstlane(base);
+        wave_lds_sync();
+        for (int i = lane; i < nbuf; i += 64)
+            if (base + i < P.ccap) out[base + i] = kbuf[i];
+        wave_lds_sync();
+        nbuf = 0;
+    };
+    int hsA = 0, hdA = 0, hsB = 0, hdB = 0;              // Sobel row terms of image rows ir-2, ir-1
+    int xA = 0, yA = 0, zA = 0, xB = 0, yB = 0, zB = 0;  // box row sums (xx, xy, yy) of rows pr-2, pr-1
+    float eA = 0.f, eB = 0.f;                            // eigen rows r-2, r-1
+    // eigen row r from the box row sums of rows r-1, r, r+1; then the NMS of row r-1
+    auto eig_row = [&](int r, int ax, int ay, int az, int bx, int by, int bz, int cx, int cy, int cz) {
+        const int sxx = ax + bx + cx, sxy = ay + by + cy, syy = az + bz + cz;
+        const int T = sxx + syy, dd = sxx - syy;
+        const double Dd = (double)dd * (double)dd + 4.0 * ((double)sxy * (double)sxy);
+        const float v = (float)(((double)T - sqrt(Dd)) * sc);
+        if (own && r >= y0 && r < m1) {
+            const uint32_t k = fkey(v);
+            kmax = k > kmax ? k : kmax;
+            if (P.eig_out) P.eig_out[(int64_t)b * W * H + (int64_t)r * W + c] = v;
+        }
+        const int rn = r - 1;
+        if (rn >= o0 && rn < o1) {
+            const int iA = __float_as_int(eA), iB = __float_as_int(eB), iV = __float_as_int(v);
+            const float mA = fmaxf(fmaxf(__int_as_float(dpp_from_left(iA)), eA), __int_as_float(dpp_from_right(iA)));
+            const float mV = fmaxf(fmaxf(__int_as_float(dpp_from_left(iV)), v), __int_as_float(dpp_from_right(iV)));
+            const float mB = fmaxf(__int_as_float(dpp_from_left(iB)), __int_as_float(dpp_from_right(iB)));
+            const bool cand = nms_col && out && eB > 0.f && eB >= fmaxf(fmaxf(mA, mV), mB);
+            const uint64_t m = __ballot(cand);
+            if (m) {
+                if (cand) {
+                    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+                    kbuf[nbuf + pre] = ((uint64_t)fkey(eB) << 32) | (uint32_t)(rn * W + c);
+                }
+                nbuf += __popcll(m);
+                if (nbuf > E3_CAP - 64) flush();
+            }
+        }
+        eA = eB;
+        eB = v;
+    };
+    for (int ir = g0 - 1; ir <= g1 + 1; ++ir) {
+        const int iv = colp[(int64_t)ir * P.pitch];
+        const int il = dpp_from_left(iv), irt = dpp_from_right(iv);
+        const int hs = il + 2 * iv + irt, hd = irt - il;
+        if (ir >= g0 + 1) {
+            const int pr = ir - 1;                       // gradient row
+            const int gx = hdA + 2 * hdB + hd, gy = hs - hsA;
+            const int pxx = gx * gx, pxy = gx * gy, pyy = gy * gy;
+            int lxx = dpp_from_left(pxx), lxy = dpp_from_left(pxy), lyy = dpp_from_left(pyy);
+            int rxx = dpp_from_right(pxx), rxy = dpp_from_right(pxy), ryy = dpp_from_right(pyy);
+            if (hedge) {                                 // boxFilter BORDER_REFLECT_101 in x
+                if (c == 0) { lxx = rxx; lxy = rxy; lyy = ryy; }
+                if (c == W - 1) { rxx = lxx; rxy = lxy; ryy = lyy; }
+            }
+            const int hx = lxx + pxx + rxx, hy = lxy + pxy + rxy, hz = lyy + pyy + ryy;
+            // eigen row pr-1 (BORDER_REFLECT_101 in y: row -1 is row 1)
+            const int r = pr - 1;
+            if (r >= e0) {
+                if (r == 0) eig_row(r, hx, hy, hz, xB, yB, zB, hx, hy, hz);
+                else eig_row(r, xA, yA, zA, xB, yB, zB, hx, hy, hz);
+            }
+            if (pr == H - 1 && pr >= e0 && pr >= 1)      // last image row: row H is row H-2
+                eig_row(pr, xB, yB, zB, hx, hy, hz, xB, yB, zB);
+            xA = xB; yA = yB; zA = zB;
+            xB = hx; yB = hy; zB = hz;
+        }
+        hsA = hsB; hdA = hdB;
+        hsB = hs; hdB = hd;
+    }
+    if (out && nbuf) flush();
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t t2 = __shfl_xor(kmax, o, 64);
+        kmax = t2 > kmax ? t2 : kmax;
+    }
+    if (lane == 0 && kmax) atomicMax(&P.eig_max[b], kmax);
+}
+
 // ---------------------------------------------------------------- GFTT selection
 #define SEL_THREADS 1024
 #define PAGE 4096
@@ -1328,19 +1534,22 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
                             int64_t frame_stride, vo_stream_t stream)
 {
     if (!d || !s || !frames || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
-    uint8_t* pyr = s->pyr[cur];
-    {
-        const int pw = d->W + 2 * VO_BORDER, ph = d->H + 2 * VO_BORDER;
-        dim3 g((pw + 1023) / 1024, (ph + 3) / 4, d->B);
-        hipLaunchKernelGGL(k_ingest, g, dim3(256), 0, VO_STREAM(stream), frames, frame_stride, pyr, d->pyr_stride,
-                           d->W, d->H, d->lvl_pitch[0], d->lvl_off[0], ph);
-    }
-    for (int l = 1; l < d->nlev; ++l) {
-        const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
-        dim3 g((pw + 4 * 64 - 1) / (4 * 64), (ph + 3) / 4, d->B);
-        hipLaunchKernelGGL(k_pyrdown, g, dim3(256), 0, VO_STREAM(stream), pyr, d->pyr_stride, d->lvl_w[l - 1],
-                           d->lvl_pitch[l - 1], d->lvl_off[l - 1], d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l],
-                           d->lvl_off[l]);
+    for (int l = 0; l < d->nlev; ++l) {
+        PyrLevelArgs A;
+        if (l == 0) {
+            A.src = frames; A.sstride = frame_stride; A.sw = A.sh = A.spitch = 0; A.soff = 0;
+        } else {
+            A.src = s->pyr[cur]; A.sstride = d->pyr_stride;
+            A.sw = d->lvl_w[l - 1]; A.sh = d->lvl_h[l - 1]; A.spitch = d->lvl_pitch[l - 1]; A.soff = d->lvl_off[l - 1];
+        }
+        A.pyr = s->pyr[cur]; A.pstride = d->pyr_stride;
+        A.der = s->der[cur]; A.dstride = d->der_stride;
+        A.w = d->lvl_w[l]; A.h = d->lvl_h[l]; A.pitch = d->lvl_pitch[l]; A.off = d->lvl_off[l];
+        A.level = l;
+        const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
+        if (A.pitch % 64 || A.pitch < pw) return VO_EARG;
+        dim3 g((pw + PT_W - 1) / PT_W, (ph + PT_H - 1) / PT_H, d->B);
+        hipLaunchKernelGGL(k_pyr_level, g, dim3(256), 0, VO_STREAM(stream), A);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
 }
@@ -1351,7 +1560,7 @@ extern "C" int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_s
     for (int l = 0; l < d->nlev; ++l) {
         const int pw = d->lvl_w[l] + 2 * VO_BORDER, ph = d->lvl_h[l] + 2 * VO_BORDER;
         dim3 g((pw + 4 * 64 - 1) / (4 * 64), (ph + 3) / 4, d->B);
-        hipLaunchKernelGGL(k_scharr, g, dim3(256), 0, VO_STREAM(stream), s->pyr[which], d->pyr_stride, s->der,
+        hipLaunchKernelGGL(k_scharr, g, dim3(256), 0, VO_STREAM(stream), s->pyr[which], d->pyr_stride, s->der[which],
                            d->der_stride, d->lvl_w[l], d->lvl_h[l], d->lvl_pitch[l], d->lvl_off[l]);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
@@ -1361,7 +1570,7 @@ static void fill_lk(LKParams& P, const vo_dims* d, const vo_opts* o, const vo_st
 {
     P.prev = s->pyr[prev];
     P.next = s->pyr[1 - prev];
-    P.der = s->der;
+    P.der = s->der[prev];
     P.pstride = d->pyr_stride;
     P.dstride = d->der_stride;
     P.L = d->nlev - 1;
@@ -1455,6 +1664,22 @@ extern "C" int vo_lk_prof_read(long long* out)
 }
 #endif
 
+// eigen + NMS pass: the row-streaming k_eig3 for blockSize 3 / min-eigenvalue (every
+// reference configuration), the tiled k_eignms otherwise (or with VO_EIG_GENERIC=1)
+static void launch_eig(EigParams E, hipStream_t st)
+{
+    static const int generic = [] { const char* e = getenv("VO_EIG_GENERIC"); return e ? atoi(e) : 0; }();
+    if (E.bs == 3 && !E.harris && !generic) {
+        E.tiles_x = (E.W + E3_OUT - 1) / E3_OUT;
+        E.tiles_y = (E.H + E3_TH - 1) / E3_TH;
+        const int total = E.B * E.tiles_x * E.tiles_y;
+        hipLaunchKernelGGL(k_eig3, dim3(((total + 7) / 8) * 8), dim3(64), 0, st, E);
+        return;
+    }
+    const int total = E.B * E.tiles_x * E.tiles_y;
+    hipLaunchKernelGGL(k_eignms, dim3(((total + 7) / 8) * 8), dim3(256), 0, st, E);
+}
+
 extern "C" int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream)
 {
     if (!d || !o || !s || cur < 0 || cur > 1) return VO_EARG;
@@ -1468,8 +1693,7 @@ extern "C" int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state
     E.B = d->B; E.tiles_x = (d->W + EIG_TW - 1) / EIG_TW; E.tiles_y = (d->H + EIG_TH - 1) / EIG_TH;
     E.chain_status = nullptr;
     E.eig_out = s->eig;
-    const int total = d->B * E.tiles_x * E.tiles_y;
-    hipLaunchKernelGGL(k_eignms, dim3(((total + 7) / 8) * 8), dim3(256), 0, st, E);
+    launch_eig(E, st);
     return hip_ok() ? VO_OK : VO_EHIP;
 }
 
@@ -1487,10 +1711,7 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
     E.B = d->B; E.tiles_x = (d->W + EIG_TW - 1) / EIG_TW; E.tiles_y = (d->H + EIG_TH - 1) / EIG_TH;
     E.chain_status = s->status;
     E.eig_out = nullptr;
-    {
-        const int total = d->B * E.tiles_x * E.tiles_y;
-        hipLaunchKernelGGL(k_eignms, dim3(((total + 7) / 8) * 8), dim3(256), 0, st, E);
-    }
+    launch_eig(E, st);
     SelParams S;
     S.keys = s->gf_keys; S.nkeys = s->gf_n; S.ccap = d->ccap; S.W = d->W; S.H = d->H;
     S.eig_max = s->eig_max; S.quality = o->feature_quality_level;

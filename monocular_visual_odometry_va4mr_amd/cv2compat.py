@@ -125,7 +125,7 @@ def calcOpticalFlowPyrLK(prevImg, nextImg, prevPts, nextPts, winSize=(21, 21), m
     eng = _engine(W, H, winSize=tuple(int(v) for v in winSize), maxLevel=int(maxLevel),
                   criteria=tuple(criteria))
     eng.opts.min_eig = float(minEigThreshold)
-    eng.build_pyramid(a, 0, deriv=True)
+    eng.build_pyramid(a, 0)
     eng.build_pyramid(b, 1)
     dev = _dev()
     if n == 0:

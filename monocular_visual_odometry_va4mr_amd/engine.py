@@ -9,7 +9,7 @@ memory and to obtain the current stream.
 
 The reference's per-frame control flow maps to stages as
 
-    feature_tracking :271-290   -> vo_pyr_build(cur) + vo_track(prev) + vo_pyr_deriv(cur)
+    feature_tracking :271-290   -> vo_pyr_build(cur) (pyramid + derivatives) + vo_track(prev)
     PnP step        :338-358    -> vo_pnp
     triangulation   :366-367    -> vo_triangulate
     feature_adding  :369        -> vo_gftt(cur) + vo_add_corners_finish (also :371-373)
@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+
+import os
 
 import numpy as np
 import torch
@@ -110,7 +112,8 @@ class Engine:
         T = {}
         T["pyr0"] = z(B, d.pyr_stride, dt=torch.uint8)
         T["pyr1"] = z(B, d.pyr_stride, dt=torch.uint8)
-        T["der"] = z(B, d.der_stride, dt=torch.int16)
+        T["der0"] = z(B, d.der_stride, dt=torch.int16)     # zero border is relied upon
+        T["der1"] = z(B, d.der_stride, dt=torch.int16)
         T["lm_X"] = z(B, ncap, 3, dt=torch.float32)
         T["lm_kp"] = z(B, ncap, 2, dt=torch.float32)
         T["nL"] = z(B, dt=torch.int32)
@@ -164,6 +167,8 @@ class Engine:
 
     # ------------------------------------------------------------------ stages
     def build_pyramid(self, frames: torch.Tensor, which: int, deriv: bool = False):
+        """Pyramid + Scharr derivatives of `frames` into pyr[which] / der[which] (vo_pyr_build
+        always produces both; deriv=True additionally recomputes der[which] by vo_pyr_deriv)."""
         frames = self._frames(frames)
         self._chk(self.lib.vo_pyr_build(self._pd, self._ps, which, C.c_void_p(frames.data_ptr()),
                                         self.W * self.H, self.stream), "vo_pyr_build")
@@ -179,7 +184,7 @@ class Engine:
             raise ValueError(f"frames must be uint8 [{self.B},{self.H},{self.W}]")
         return frames.to(self.device, non_blocking=True).contiguous()
 
-    STAGES = ("pyr_build", "track", "pyr_deriv", "pnp", "triangulate", "gftt", "add_finish")
+    STAGES = ("pyr_build", "track", "pnp", "triangulate", "gftt", "add_finish")
 
     def step(self, frames, marks=None):
         """One continuous_operation for every chain (frames: uint8 [B,H,W], any device).
@@ -192,16 +197,18 @@ class Engine:
         self.prev = 1 - self.prev
 
     def _side_stream(self):
+        if os.environ.get("VO_ONE_STREAM") == "1":      # profiling: every stage on the main stream
+            return torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         return self._side
 
     def _step_launch(self, frames, prev, marks=None):
-        """Stage DAG of one step on two streams.  main: pyramid(cur) -> track(prev) -> PnP ->
-        triangulate -> [join] -> add_finish.  side: GFTT on the new frame (needs only its
-        pyramid, VisualOdometryPipeLine.py:253) and, once tracking has read the previous
-        frame's derivatives, the new frame's Scharr derivatives -- both overlap PnP.  GFTT
-        never writes the chain status (PnP owns it while the two run; see k_gftt_select)."""
+        """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
+        new frame (pyr[cur], der[cur]) -> track(prev) -> PnP -> triangulate -> [join] ->
+        add_finish.  side: GFTT on the new frame (needs only its pyramid,
+        VisualOdometryPipeLine.py:253), overlapping tracking and PnP.  GFTT never writes the
+        chain status (PnP owns it while the two run; see k_gftt_select)."""
         cur = 1 - prev
         lib = self.lib
         main = torch.cuda.current_stream(self.device)
@@ -220,14 +227,12 @@ class Engine:
 
         run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
         side.wait_stream(main)                                    # pyramid(cur) ready
-        run(5, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
+        run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
-        side.wait_stream(main)                                    # der(prev) consumed
-        run(2, side, lambda: lib.vo_pyr_deriv(pd, ps, cur, ss))
-        run(3, main, lambda: lib.vo_pnp(pd, po, ps, sm))
-        run(4, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
-        main.wait_stream(side)                                    # corners + der(cur) ready
-        run(6, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))
+        run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
+        run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
+        main.wait_stream(side)                                    # corners ready
+        run(5, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))
 
     def capture_step(self):
         """Capture the two ping-pong variants of the step into hipGraphs; returns a
@@ -309,7 +314,7 @@ class Engine:
                                         C.c_void_p(pts1.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, st),
                   "vo_bootstrap")
         self.prev = 0
-        self.build_pyramid(img1, self.prev, deriv=True)
+        self.build_pyramid(img1, self.prev)
         self._boot_debug = {"kp0": kp0, "kp1": kp1, "n0": n0, "n1": n1, "idx2": idx2, "dist2": dist2,
                             "pts0": pts0, "pts1": pts1, "cnt": cnt}
 
@@ -347,12 +352,12 @@ class Engine:
         # rebuild the potential_frame pyramid + derivatives for this chain only
         full = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=dev)
         full[b] = img
-        keep = T["pyr%d" % self.prev].clone(), T["der"].clone()
-        self.build_pyramid(full, self.prev, deriv=True)
+        keep = T["pyr%d" % self.prev].clone(), T["der%d" % self.prev].clone()
+        self.build_pyramid(full, self.prev)
         mask = torch.zeros(self.B, dtype=torch.bool, device=dev)
         mask[b] = True
         T["pyr%d" % self.prev][~mask] = keep[0][~mask]
-        T["der"][~mask] = keep[1][~mask]
+        T["der%d" % self.prev][~mask] = keep[1][~mask]
 
     def export_chain(self, b: int) -> dict:
         T = self.t
@@ -380,8 +385,10 @@ class Engine:
         buf = self.t["pyr%d" % which][b, o:o + (h + 2 * L.VO_BORDER) * p].view(h + 2 * L.VO_BORDER, p)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()
 
-    def deriv_level(self, level: int, b: int = 0) -> np.ndarray:
+    def deriv_level(self, level: int, b: int = 0, which: int | None = None) -> np.ndarray:
+        """Scharr (dx, dy) of pyramid `which` (default: the potential_frame's, pyr[prev])."""
         d = self.dims
+        which = self.prev if which is None else which
         w, h, p, o = d.lvl_w[level], d.lvl_h[level], d.lvl_pitch[level], d.lvl_off[level]
-        buf = self.t["der"][b, 2 * o:2 * (o + (h + 2 * L.VO_BORDER) * p)].view(h + 2 * L.VO_BORDER, p, 2)
+        buf = self.t["der%d" % which][b, 2 * o:2 * (o + (h + 2 * L.VO_BORDER) * p)].view(h + 2 * L.VO_BORDER, p, 2)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()

@@ -28,7 +28,7 @@ def main():
     eng = Engine(g["K"], opts, W, H, batch=1, ncap=8192, pcap=8192, fcap=64)
     bad = 0
     for i in range(lo, hi - 1):
-        eng.build_pyramid(fr[i], 0, deriv=True)
+        eng.build_pyramid(fr[i], 0)
         eng.build_pyramid(fr[i + 1], 1)
         assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
         torch.cuda.synchronize()

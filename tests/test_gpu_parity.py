@@ -40,17 +40,66 @@ def test_library_is_gfx950():
 
 
 def test_pyramid_scharr_bitexact(kitti_frames, engine_factory):
+    """vo_pyr_build (fused pyramid level + Scharr pass) vs the oracle's pyrDown / Scharr, and
+    vo_pyr_deriv (standalone Scharr) vs the fused derivatives."""
     from oracle import _olib as O
     fr, K = kitti_frames
     eng, opts = engine_factory(K=K)
-    eng.build_pyramid(fr[0], 0, deriv=True)
+    eng.build_pyramid(fr[0], 0)
     torch.cuda.synchronize()
     ref = fr[0]
+    fused = []
     for lv in range(eng.dims.nlev):
         got = eng.pyramid_level(0, lv)
         assert np.array_equal(got, ref), f"pyramid level {lv}"
-        assert np.array_equal(eng.deriv_level(lv), O.scharr(ref)), f"scharr level {lv}"
+        fused.append(eng.deriv_level(lv, which=0))
+        assert np.array_equal(fused[-1], O.scharr(ref)), f"scharr level {lv}"
         ref = O.pyrdown(ref)
+    assert eng.lib.vo_pyr_deriv(eng._pd, eng._ps, 0, eng.stream) == 0
+    torch.cuda.synchronize()
+    for lv in range(eng.dims.nlev):
+        assert np.array_equal(eng.deriv_level(lv, which=0), fused[lv]), f"vo_pyr_deriv level {lv}"
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (1024, 768), (131, 67), (300, 37), (45, 300)])
+def test_pyramid_scharr_sizes(engine_factory, W, H):
+    """Odd sizes (tile edges, reflect-101 corners, small levels) and two chains per launch;
+    the derivative border must stay zero and the pyramid border reflect-101."""
+    from oracle import _olib as O
+    from monocular_visual_odometry_va4mr_amd import _lib as L
+    rng = np.random.default_rng(W * H)
+    imgs = rng.integers(0, 256, (2, H, W), dtype=np.uint8)
+    K = np.array([[300.0, 0, W / 2], [0, 300.0, H / 2], [0, 0, 1]])
+    eng, _ = engine_factory(K=K, B=2, W=W, H=H)
+    eng.build_pyramid(torch.from_numpy(imgs), 1)
+    torch.cuda.synchronize()
+    d = eng.dims
+    Bd = L.VO_BORDER
+    for b in range(2):
+        ref = imgs[b]
+        for lv in range(d.nlev):
+            assert np.array_equal(eng.pyramid_level(1, lv, b), ref), f"b={b} pyramid level {lv}"
+            w, h, p, o = d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv]
+            full = eng.t["der1"][b, 2 * o:2 * (o + (h + 2 * Bd) * p)].view(h + 2 * Bd, p, 2).cpu().numpy()
+            assert np.array_equal(full[Bd:Bd + h, Bd:Bd + w], O.scharr(ref)), f"b={b} scharr level {lv}"
+            inner = np.zeros(full.shape[:2], bool)
+            inner[Bd:Bd + h, Bd:Bd + w] = True
+            inner[:, w + 2 * Bd:] = True          # pitch slack: don't care
+            assert not full[~inner].any(), f"b={b} derivative border level {lv}"
+            pp = eng.t["pyr1"][b, o:o + (h + 2 * Bd) * p].view(h + 2 * Bd, p).cpu().numpy()[:, :w + 2 * Bd]
+            ry = [O_refl(i - Bd, h) for i in range(h + 2 * Bd)]
+            rx = [O_refl(i - Bd, w) for i in range(w + 2 * Bd)]
+            assert np.array_equal(pp, ref[np.ix_(ry, rx)]), f"b={b} reflect-101 border level {lv}"
+            ref = O.pyrdown(ref)
+
+
+def O_refl(p, n):
+    """cv::borderInterpolate(BORDER_REFLECT_101)"""
+    if n == 1:
+        return 0
+    while p < 0 or p >= n:
+        p = -p if p < 0 else 2 * n - p - 2
+    return p
 
 
 def test_gftt_bitexact(kitti_frames, engine_factory):
@@ -82,7 +131,7 @@ def test_lk_bitexact(kitti_frames, engine_factory):
     # tiny sub-pixel offsets make OpenCV's iw11 = 2^14 - iw00 - iw01 - iw10 negative
     tiny = (pts[:200] + np.float32([[1e-3, 2e-3]]) * rng.integers(1, 8, (min(200, len(pts)), 2))).astype(np.float32)
     pts = np.concatenate([pts, extra, tiny])
-    eng.build_pyramid(fr[0], 0, deriv=True)
+    eng.build_pyramid(fr[0], 0)
     eng.build_pyramid(fr[1], 1)
     n = len(pts)
     dpts = torch.from_numpy(pts).cuda().reshape(1, n, 2)
