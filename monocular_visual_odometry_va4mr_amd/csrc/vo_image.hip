@@ -83,12 +83,26 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         if (x >= 0) { atomicMin(&mm[2], x); atomicMax(&mm[3], x); }
     }
     __syncthreads();
+    // every load of a phase is issued before the first one is consumed (fixed trip counts,
+    // unrolled): the staging is latency-bound otherwise
+    constexpr int NPV = (PV_H * PV_W + 255) / 256;
     if (A.level == 0) {
         const uint8_t* fr = A.src + (int64_t)b * A.sstride;
-        for (int e = tid; e < PV_H * PV_W; e += 256) {
-            const int k = e / PV_W, c = e - k * PV_W;
+        uint32_t v[NPV];
+#pragma unroll
+        for (int i = 0; i < NPV; ++i) {
+            const int e = tid + 256 * i;
+            // unconditional load from a clamped address (keeps the loads in one batch)
+            const int ee = min(e, PV_H * PV_W - 1);
+            const int k = ee / PV_W, c = ee - k * PV_W;
             const int y = yk[k], x = xc[c];
-            PV[e] = (y >= 0 && x >= 0) ? fr[(int64_t)y * A.w + x] : 0;
+            v[i] = fr[(int64_t)max(y, 0) * A.w + max(x, 0)];
+            if (y < 0 || x < 0) v[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < NPV; ++i) {
+            const int e = tid + 256 * i;
+            if (e < PV_H * PV_W) PV[e] = (uint8_t)v[i];
         }
     } else {
         // source rectangle (level l-1 coordinates) under the tile
@@ -99,10 +113,19 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         const int ax0 = gx0 & ~3, sh = gx0 - ax0;
         const int nwd = (sx1 + VO_BORDER - ax0) / 4 + 1; // dwords per staged row
         const uint8_t* sbase = A.src + (int64_t)b * A.sstride + A.soff + ax0;
-        for (int e = tid; e < nsr * nwd; e += 256) {
-            const int r = e / nwd, c = e - r * nwd;
-            SRw[r * (PS_W / 4) + c] =
-                *(const uint32_t*)(sbase + (int64_t)(sy0 + r + VO_BORDER) * A.spitch + 4 * c);
+        constexpr int NSR = (PS_H * (PS_W / 4) + 255) / 256;
+        uint32_t v[NSR];
+#pragma unroll
+        for (int i = 0; i < NSR; ++i) {
+            const int e = tid + 256 * i;
+            const int r = e / (PS_W / 4), c = e - r * (PS_W / 4);
+            const bool in = r < nsr && c < nwd;
+            v[i] = *(const uint32_t*)(sbase + (int64_t)(sy0 + (in ? r : 0) + VO_BORDER) * A.spitch + 4 * (in ? c : 0));
+        }
+#pragma unroll
+        for (int i = 0; i < NSR; ++i) {
+            const int e = tid + 256 * i;
+            if (e < PS_H * (PS_W / 4)) SRw[e] = v[i];
         }
         __syncthreads();
         // horizontal [1 4 6 4 1] at the tile's columns, every staged row
