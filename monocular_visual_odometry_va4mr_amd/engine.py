@@ -91,8 +91,10 @@ class Engine:
         d.nlev = nlev
         off = 0
         w, h = self.W, self.H
+        # one pitch for every level (that of level 0): the LK kernel addresses rows of any
+        # level with scalar offsets r * pitch
+        pitch = ((self.W + 2 * L.VO_BORDER + 63) // 64) * 64
         for lv in range(nlev):
-            pitch = ((w + 2 * L.VO_BORDER + 63) // 64) * 64
             d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv] = w, h, pitch, off
             off += (h + 2 * L.VO_BORDER) * pitch
             w, h = (w + 1) // 2, (h + 1) // 2
@@ -390,5 +392,8 @@ class Engine:
         d = self.dims
         which = self.prev if which is None else which
         w, h, p, o = d.lvl_w[level], d.lvl_h[level], d.lvl_pitch[level], d.lvl_off[level]
-        buf = self.t["der%d" % which][b, 2 * o:2 * (o + (h + 2 * L.VO_BORDER) * p)].view(h + 2 * L.VO_BORDER, p, 2)
+        n = (h + 2 * L.VO_BORDER) * p
+        t = self.t["der%d" % which][b]
+        planes = [t[q * d.pyr_stride + o:q * d.pyr_stride + o + n].view(h + 2 * L.VO_BORDER, p) for q in (0, 1)]
+        buf = torch.stack(planes, dim=-1)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()
