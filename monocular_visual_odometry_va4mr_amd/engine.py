@@ -227,13 +227,16 @@ class Engine:
             if marks is not None:
                 marks(i, True, strm)
 
+        forked = side.cuda_stream != main.cuda_stream
         run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
-        side.wait_stream(main)                                    # pyramid(cur) ready
+        if forked:
+            side.wait_stream(main)                                # pyramid(cur) ready
         run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
         run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
         run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
-        main.wait_stream(side)                                    # corners ready
+        if forked:
+            main.wait_stream(side)                                # corners ready
         run(5, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))
 
     def capture_step(self):
