@@ -285,6 +285,26 @@ VO_DEV bool lk_block(int B, int nb, int& b, int& pb, bool xcd = true)
 // over the 14-bit weights split into 7+7 bits; all window sums are integer and exact, so
 // results match the CPU restatement bit for bit.
 #define LK_M 4
+// a zero the compiler cannot see through: per-lane index math that uses it is recomputed at
+// each staging instead of being hoisted out of the point / level loops into live VGPRs
+VO_DEV int opaque0()
+{
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+// buffer resource over one chain's buffer: loads take 32-bit offsets (one VGPR, not a 64-bit
+// address) and read zeros outside [0, bytes) instead of faulting
+VO_DEV __amdgpu_buffer_rsrc_t lkq_rsrc(const void* base, int64_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+#ifndef LK_JPRE
+#define LK_JPRE 1
+#endif
+#ifndef LK_QTC
+#define LK_QTC 3            // QT build: LDS reads batched over this many trips
+#endif
 VO_DEV void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -522,6 +542,14 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 #else
 #define LKCHK(ptr, base, bytes, what) true
 #endif
+#ifdef VO_LK_CHECK
+// offset form for the buffer loads of k_lk_w (which read zeros past the chain's buffer)
+#define LKCHKO(off, bytes, what) \
+    do { if ((off) < 0 || (int64_t)(off) + 4 > (int64_t)(bytes)) \
+        printf("LKCHK %s b=%d p=%d level=%d off=%lld size=%lld\n", what, b, pcur, level, (long long)(off), (long long)(bytes)); } while (0)
+#else
+#define LKCHKO(off, bytes, what) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------------------
 // k_lk_w<WW, WH>: the same LK level as k_lk for a compile-time window (the reference uses
@@ -560,42 +588,88 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     if (n1 <= P.seg1_min) n1 = 0;
     const int ntot = n0 + n1;
     const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
-    int wyv[MAXJ], wxv[MAXJ];
+    // window pixel k = lane + 64 j; its offset in the QT tile is kept (the iterations read it),
+    // its row / column are recomputed where needed
+    int toff[MAXJ];
     bool live[MAXJ];
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
         const int k = lane + 64 * j;
         live[j] = k < NPX;
-        wyv[j] = live[j] ? k / WW : 0;
-        wxv[j] = live[j] ? k - (k / WW) * WW : 0;
+        toff[j] = live[j] ? (k / WW) * TW + k % WW : 0;
     }
     int tx0 = 0, ty0 = 0, jsh = 0;
-    int cols = 0, rows = 0, pitch = 0;
-    const uint8_t* I = nullptr;
-    const int16_t* DI = nullptr;
-    const uint8_t* J = nullptr;
-    // (re)stage the J tile so that it covers the window at (inx, iny)
-    auto stage_j = [&](int inx, int iny) {
+    int cols = 0, rows = 0, pitch = 0, loff = 0;
+    const __amdgpu_buffer_rsrc_t rI = lkq_rsrc(P.prev + (int64_t)b * P.pstride, P.pstride);
+    const __amdgpu_buffer_rsrc_t rJ = lkq_rsrc(P.next + (int64_t)b * P.pstride, P.pstride);
+    const __amdgpu_buffer_rsrc_t rDX = lkq_rsrc(P.der + (int64_t)b * P.dstride, 2 * P.dplane);
+    const __amdgpu_buffer_rsrc_t rDY = lkq_rsrc(P.der + (int64_t)b * P.dstride + P.dplane, 2 * P.dplane);
+    // Staging is split into issue (global loads into registers, fixed unrolled trip counts)
+    // and store (LDS writes), so that every load of a stage is in flight at once: one memory
+    // round trip per stage instead of one per loop trip.
+    constexpr int NIR = ((WH + 1) * IRW + 63) / 64, NDR = ((WH + 1) * DRW + 63) / 64;
+    constexpr int NJR = ((TH + 1) * JRW + 63) / 64, NQT = (TH * TW + 63) / 64;
+    // J tile origin covering the window at (inx, iny)
+    auto j_origin = [&](int inx, int iny) {
         tx0 = max(inx - LK_M, -VO_BORDER);
         ty0 = min(max(iny - LK_M, -VO_BORDER), rows + VO_BORDER - 1 - TH);
+        jsh = (tx0 + VO_BORDER) & 3;
+    };
+    auto j_issue = [&](uint32_t (&v)[NJR]) {
         const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
-        jsh = gx0 & 3;
-        const uint8_t* rowp = J + (int64_t)gy0 * pitch + (gx0 & ~3);
+        const int base = loff + gy0 * pitch + (gx0 & ~3);          // wave-uniform
+        const int ln = lane + opaque0();
+#pragma unroll
+        for (int k = 0; k < NJR; ++k) {
+            const int q = ln + 64 * k;
+            v[k] = 0u;
+            if (q < (TH + 1) * JRW) {
+                const int r = q / JRW, c = q - r * JRW;
+                const int o = r * pitch + 4 * c;
+                LKCHKO(base + o, P.pstride, "J");
+                v[k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, o, base, 0);
+            }
+        }
+    };
+    // JR rows -> LDS, then the packed 2x2 quads QT (LDS -> LDS, reads batched 3 trips at a time)
+    auto j_store = [&](const uint32_t (&v)[NJR]) {
+#pragma unroll
+        for (int k = 0; k < NJR; ++k) {
+            const int q = lane + 64 * k;
+            if (q < (TH + 1) * JRW) JR[q] = v[k];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int k0 = 0; k0 < NQT; k0 += LK_QTC) {
+            uint32_t t0[LK_QTC], t1[LK_QTC], t2[LK_QTC], t3[LK_QTC];
+            const int ln = lane + opaque0();
+#pragma unroll
+            for (int i = 0; i < LK_QTC; ++i) {
+                const int q = ln + 64 * (k0 + i);
+                t0[i] = t1[i] = t2[i] = t3[i] = 0u;
+                if (k0 + i < NQT && q < TH * TW) {
+                    const int r = q / TW, c = q - r * TW;
+                    const uint8_t* s = jr8 + r * (4 * JRW) + jsh + c;
+                    t0[i] = s[0]; t1[i] = s[1]; t2[i] = s[4 * JRW]; t3[i] = s[4 * JRW + 1];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < LK_QTC; ++i) {
+                const int q = lane + 64 * (k0 + i);
+                if (k0 + i < NQT && q < TH * TW) QT[q] = t0[i] | (t1[i] << 8) | (t2[i] << 16) | (t3[i] << 24);
+            }
+        }
+        wave_lds_sync();
+    };
+    // (re)stage the J tile so that it covers the window at (inx, iny)
+    auto stage_j = [&](int inx, int iny) {
         LKPROF_ADD(3, 1);
         LKPROF_T(tj0);
+        j_origin(inx, iny);
+        uint32_t v[NJR];
+        j_issue(v);
         wave_lds_sync();
-        for (int q = lane; q < (TH + 1) * JRW; q += 64) {
-            const int r = q / JRW, c = q - r * JRW;
-            const uint8_t* ja = rowp + (int64_t)r * pitch + 4 * c;
-            JR[q] = LKCHK(ja, P.next + (int64_t)b * P.pstride, P.pstride, "J") ? *(const uint32_t*)ja : 0u;
-        }
-        wave_lds_sync();
-        for (int q = lane; q < TH * TW; q += 64) {
-            const int r = q / TW, c = q - r * TW;
-            const uint8_t* s = jr8 + r * (4 * JRW) + jsh + c;
-            QT[q] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[4 * JRW] << 16) | ((uint32_t)s[4 * JRW + 1] << 24);
-        }
-        wave_lds_sync();
+        j_store(v);
         LKPROF_T(tj1);
         LKPROF_ADD(6, tj1 - tj0);
     };
@@ -619,10 +693,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
         float errv = 0.f;
         float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
         for (level = level_hi; level >= level_lo; --level) {
-        cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level];
-        I = P.prev + b * P.pstride + P.loff[level];
-        DI = P.der + b * P.dstride + P.loff[level];
-        J = P.next + b * P.pstride + P.loff[level];
+        cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level]; loff = (int)P.loff[level];
         const float sc = (float)(1. / (1 << level));
         float px = ptx * sc, py = pty * sc;
         if (level == P.L) { ox = px; oy = py; }
@@ -641,28 +712,62 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 if (level == 0) { status = 0; errv = 0.f; }
                 break;
             }
-            // stage I (u8) and dI (int16 x2) rows under the window
+            // stage I (u8) and dI (int16 x2) rows under the window, together with the J tile
+            // of the first iteration (same bounds test as the iteration's): one round trip
             bool staged = false;
             {
                 LKPROF_T(ti0);
                 const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
                 const int ish = gx & 3;
-                const uint8_t* irow = I + (int64_t)gy * pitch + (gx & ~3);
-                const int16_t* drow = DI + (int64_t)gy * pitch + gx;     // dx plane; dy at +dplane
-                wave_lds_sync();
-                for (int q = lane; q < (WH + 1) * IRW; q += 64) {
-                    const int r = q / IRW, c = q - r * IRW;
-                    const uint8_t* ia = irow + (int64_t)r * pitch + 4 * c;
-                    IR[q] = LKCHK(ia, P.prev + (int64_t)b * P.pstride, P.pstride, "I") ? *(const uint32_t*)ia : 0u;
+                const int ibase = loff + gy * pitch + (gx & ~3);           // wave-uniform byte offsets
+                const int dbase = 2 * (loff + gy * pitch + gx);             // dx plane; dy at +2 * dplane
+                uint32_t vir[NIR], vdx[NDR], vdy[NDR], vjr[NJR];
+                const int ln = lane + opaque0();
+#pragma unroll
+                for (int k = 0; k < NIR; ++k) {
+                    const int q = ln + 64 * k;
+                    vir[k] = 0u;
+                    if (q < (WH + 1) * IRW) {
+                        const int r = q / IRW, c = q - r * IRW;
+                        const int o = r * pitch + 4 * c;
+                        LKCHKO(ibase + o, P.pstride, "I");
+                        vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, o, ibase, 0);
+                    }
                 }
-                for (int q = lane; q < (WH + 1) * DRW; q += 64) {
-                    const int r = q / DRW, c = q - r * DRW;
-                    const int16_t* da = drow + (int64_t)r * pitch + c;
-                    DR[q] = LKCHK(da, P.der + (int64_t)b * P.dstride, 2 * P.dplane, "Dx") &&
-                                    LKCHK(da + P.dplane, P.der + (int64_t)b * P.dstride + P.dplane, 2 * P.dplane, "Dy")
-                                ? (uint32_t)(uint16_t)da[0] | ((uint32_t)(uint16_t)da[P.dplane] << 16) : 0u;
+#pragma unroll
+                for (int k = 0; k < NDR; ++k) {
+                    const int q = ln + 64 * k;
+                    vdx[k] = vdy[k] = 0u;
+                    if (q < (WH + 1) * DRW) {
+                        const int r = q / DRW, c = q - r * DRW;
+                        const int o = 2 * (r * pitch + c);
+                        LKCHKO(dbase + o, 2 * P.dplane, "Dx");
+                        vdx[k] = __builtin_amdgcn_raw_buffer_load_b16(rDX, o, dbase, 0);
+                        vdy[k] = __builtin_amdgcn_raw_buffer_load_b16(rDY, o, dbase, 0);
+                    }
+                }
+                {
+                    const int jx = (int)floorf(ox - hx), jy = (int)floorf(oy - hy);
+                    staged = LK_JPRE && !(jx < -WW || jx >= cols || jy < -WH || jy >= rows) && P.max_count > 0;
+                    if (staged) {
+                        LKPROF_ADD(3, 1);
+                        j_origin(jx, jy);
+                        j_issue(vjr);
+                    }
                 }
                 wave_lds_sync();
+#pragma unroll
+                for (int k = 0; k < NIR; ++k) {
+                    const int q = lane + 64 * k;
+                    if (q < (WH + 1) * IRW) IR[q] = vir[k];
+                }
+#pragma unroll
+                for (int k = 0; k < NDR; ++k) {
+                    const int q = lane + 64 * k;
+                    if (q < (WH + 1) * DRW) DR[q] = vdx[k] | (vdy[k] << 16);
+                }
+                if (staged) j_store(vjr);      // syncs
+                else wave_lds_sync();
                 LKPROF_T(ti1);
                 LKPROF_ADD(4, ti1 - ti0);
                 float a = px - ipx, bb = py - ipy;
@@ -674,8 +779,10 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 int a11 = 0, a12 = 0, a22 = 0;
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
-                    const uint8_t* s = ir8 + wyv[j] * (4 * IRW) + ish + wxv[j];
-                    const uint32_t* d = DR + wyv[j] * DRW + wxv[j];
+                    const int kk = lane + opaque0() + 64 * j;
+                    const int wy = live[j] ? kk / WW : 0, wx = live[j] ? kk - (kk / WW) * WW : 0;
+                    const uint8_t* s = ir8 + wy * (4 * IRW) + ish + wx;
+                    const uint32_t* d = DR + wy * DRW + wx;
                     const uint32_t d00 = d[0], d01 = d[1], d10 = d[DRW], d11 = d[DRW + 1];
                     const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
                                           __mul24((int)s[4 * IRW], iw10) + __mul24((int)s[4 * IRW + 1], iw11), 9);
@@ -728,7 +835,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     int b1 = 0, b2 = 0;
 #pragma unroll
                     for (int j = 0; j < MAXJ; ++j) {
-                        const uint32_t q = tb[wyv[j] * TW + wxv[j]];
+                        const uint32_t q = tb[toff[j]];
                         uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
                                        __builtin_amdgcn_udot4(q, wlo, 256u, false);
                         if (neg) sum -= q >> 24;
@@ -783,7 +890,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     int es = 0;
 #pragma unroll
                     for (int j = 0; j < MAXJ; ++j) {
-                        const uint32_t q = tb[wyv[j] * TW + wxv[j]];
+                        const uint32_t q = tb[toff[j]];
                         uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
                                        __builtin_amdgcn_udot4(q, wlo, 256u, false);
                         if (neg) sum -= q >> 24;
@@ -847,10 +954,6 @@ VO_DEV int64_t row_sum16_split(int p)
 {
     const int lo = p & 0xFFFF, hi = p >> 16;
     return (int64_t)row_sum16(hi) * 65536 + (int64_t)row_sum16(lo);
-}
-VO_DEV __amdgpu_buffer_rsrc_t lkq_rsrc(const void* base, int64_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
 
 __global__ void __launch_bounds__(64) k_lk_q(LKParams P, int B, int nb)
