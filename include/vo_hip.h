@@ -222,6 +222,16 @@ int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t
 int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt,
                int32_t qcap, int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream);
 
+/* Batched BFMatcher().knnMatch(q, t, k=2) (:36,229) for B independent problems on MFMA
+ * (csrc/vo_match.hip): q [B][qcap][128], t [B][tcap][128] integer-valued float descriptors
+ * (SIFT: 0..255), device counts nq[B] / nt[B]; idx2 [B][qcap][2] (-1 if absent), dist2
+ * [B][qcap][2] (FLT_MAX if absent); rows >= nq[b] untouched.  Same (distance, index) order and
+ * float distances as vo_bf_knn2 / OpenCV.  scratch: device bytes >= vo_bf_knn2_batch_scratch(). */
+int64_t vo_bf_knn2_batch_scratch(int B, int32_t qcap, int32_t tcap);
+int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_t qcap, const float* t,
+                     const int32_t* nt, int32_t tcap, int32_t dim, int32_t* idx2, float* dist2,
+                     void* scratch, int64_t scratch_bytes, vo_stream_t stream);
+
 /* Ratio test + match gathering of initial_feature_matching (:218-245) for B chains:
  * keeps query i iff dist0 < ratio * dist1 (in double, as Python), in query order. */
 int vo_ratio_matches(int B, const float* kp0, const float* kp1, int32_t kp_stride,

@@ -149,6 +149,8 @@ def _declare(L):
         "vo_find_essential": ([O, C.c_int, P, P, P, i32, f64, f64, i32, P, P, P, P, i32, P], C.c_int),
         "vo_recover_pose": ([O, C.c_int, P, P, P, P, i32, P, P, P, P, P], C.c_int),
         "vo_bootstrap": ([D, O, S, P, P, P, i32, P], C.c_int),
+        "vo_bf_knn2_batch_scratch": ([C.c_int, i32, i32], i64),
+        "vo_bf_knn2_batch": ([C.c_int, P, P, i32, P, P, i32, i32, P, P, P, i64, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -166,7 +168,7 @@ def exported_symbols():
     import re
     hdr = os.path.join(os.path.dirname(_HERE), "include", "vo_hip.h")
     txt = open(hdr).read()
-    return sorted(set(re.findall(r"^\s*(?:const char\*|int)\s+(vo_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int|int64_t)\s+(vo_\w+)\s*\(", txt, re.M)))
 
 
 def check(rc: int, what: str):

@@ -59,8 +59,54 @@ class Sift:
         return self.t["kp_out"][:n].cpu().numpy(), self.t["desc"][:n].cpu().numpy()
 
 
+_SCRATCH: dict = {}
+
+
+def _scratch(dev, nbytes: int) -> torch.Tensor:
+    """Matcher scratch per device, grown on demand (kept so repeated calls do not allocate)."""
+    buf = _SCRATCH.get(dev)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        _SCRATCH[dev] = buf
+    return buf
+
+
+def bf_knn2_batch(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor):
+    """k=2 nearest neighbours for B problems on MFMA (vo_bf_knn2_batch).
+    q [B,qcap,128] / t [B,tcap,128] float32 integer-valued descriptors, nq / nt int32 [B] device
+    counts; returns idx2 [B,qcap,2] i32 (-1 absent), dist2 [B,qcap,2] f32 (FLT_MAX absent)."""
+    if q.dim() != 3 or t.dim() != 3 or q.shape[2] != 128 or t.shape[2] != 128 or q.shape[0] != t.shape[0]:
+        raise ValueError("q, t must be float32 [B, cap, 128] with the same B")
+    dev = q.device
+    B, qcap, tcap = int(q.shape[0]), int(q.shape[1]), int(t.shape[1])
+    q = q.contiguous()
+    t = t.contiguous()
+    idx2 = torch.full((B, qcap, 2), -1, dtype=torch.int32, device=dev)
+    dist2 = torch.full((B, qcap, 2), float(np.finfo(np.float32).max), dtype=torch.float32, device=dev)
+    lib = L.lib()
+    nbytes = int(lib.vo_bf_knn2_batch_scratch(B, qcap, tcap))
+    if nbytes <= 0:
+        raise ValueError("bad matcher sizes")
+    scr = _scratch(dev, nbytes)
+    st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    L.check(lib.vo_bf_knn2_batch(B, C.c_void_p(q.data_ptr()), C.c_void_p(nq.data_ptr()), qcap,
+                                 C.c_void_p(t.data_ptr()), C.c_void_p(nt.data_ptr()), tcap, 128,
+                                 C.c_void_p(idx2.data_ptr()), C.c_void_p(dist2.data_ptr()),
+                                 C.c_void_p(scr.data_ptr()), nbytes, st), "vo_bf_knn2_batch")
+    return idx2, dist2
+
+
 def bf_knn2(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor, qcap: int):
-    """k=2 nearest neighbours (device counts), returns idx2 [qcap,2] i32, dist2 [qcap,2] f32."""
+    """k=2 nearest neighbours of one problem (device counts), returns idx2 [qcap,2] i32,
+    dist2 [qcap,2] f32: the batched MFMA matcher with B = 1."""
+    q = q[:qcap]
+    i2, d2 = bf_knn2_batch(q[None], nq.reshape(1), t[None], nt.reshape(1))
+    return i2[0], d2[0]
+
+
+def bf_knn2_reference(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor, qcap: int):
+    """The single-problem kernel (vo_bf_knn2: one wave per 32 queries, train rows read from
+    global memory); kept as the second device implementation the batched one is tested against."""
     dev = q.device
     idx2 = torch.full((qcap, 2), -1, dtype=torch.int32, device=dev)
     dist2 = torch.full((qcap, 2), float(np.finfo(np.float32).max), dtype=torch.float32, device=dev)

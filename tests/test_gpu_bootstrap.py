@@ -26,6 +26,54 @@ def test_bf_knn2_exact():
                 assert dm.trainIdx == idx[i, j] and np.float32(dm.distance) == dist[i, j]
 
 
+def test_bf_knn2_batch_exact():
+    """Batched MFMA matcher vs the C restatement: ragged / empty problems, an exact tie, and
+    0/255 descriptors whose distances^2 pass 2^22 (the exact float-order fixup path)."""
+    from oracle import _olib as O
+    from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch, bf_knn2_reference
+    rng = np.random.default_rng(1)
+    qcap, tcap = 700, 900
+    sizes = [(700, 900), (1, 2), (0, 5), (333, 1), (650, 0), (129, 64), (300, 257)]
+    B = len(sizes)
+    q = np.zeros((B, qcap, 128), np.float32)
+    t = np.zeros((B, tcap, 128), np.float32)
+    for b, (nq, nt) in enumerate(sizes):
+        if b == 6:      # 0/255 descriptors, mostly opposite: d2 = 65025 * hamming >= 2^22
+            q[b, :nq] = 255 * (rng.random((nq, 128)) < 0.9)
+            t[b, :nt] = 255 * (rng.random((nt, 128)) < 0.1)
+        else:
+            q[b, :nq] = rng.integers(0, 256, (nq, 128))
+            t[b, :nt] = rng.integers(0, 256, (nt, 128))
+        if nt > 10 and nq > 3:
+            t[b, 7] = t[b, 5]          # exact tie: the lower train index must win
+            q[b, 3] = t[b, 5]
+    dev = torch.device("cuda")
+    nq_d = torch.tensor([s[0] for s in sizes], dtype=torch.int32, device=dev)
+    nt_d = torch.tensor([s[1] for s in sizes], dtype=torch.int32, device=dev)
+    idx2, dist2 = bf_knn2_batch(torch.from_numpy(q).to(dev), nq_d, torch.from_numpy(t).to(dev), nt_d)
+    idx2, dist2 = idx2.cpu().numpy(), dist2.cpu().numpy()
+    big = 0
+    for b, (nq, nt) in enumerate(sizes):
+        if nq == 0:
+            assert (idx2[b] == -1).all()
+            continue
+        if nt == 0:
+            assert (idx2[b, :nq] == -1).all() and (dist2[b, :nq] == np.finfo(np.float32).max).all()
+            continue
+        ei, ed = O.bf_knn2(np.ascontiguousarray(q[b, :nq]), np.ascontiguousarray(t[b, :nt]))
+        k = min(2, nt)
+        assert np.array_equal(idx2[b, :nq, :k], ei[:, :k]), f"problem {b}"
+        assert np.array_equal(dist2[b, :nq, :k], ed[:, :k]), f"problem {b}"
+        if nt < 2:
+            assert (idx2[b, :nq, 1] == -1).all()
+        big += int((ed[:, 1] >= 2048.0).sum())
+        # the single-problem kernel agrees as well
+        ri, rd = bf_knn2_reference(torch.from_numpy(q[b]).to(dev), nq_d[b:b + 1], torch.from_numpy(t[b]).to(dev),
+                                   nt_d[b:b + 1], qcap)
+        assert np.array_equal(ri.cpu().numpy()[:nq, :k], ei[:, :k])
+    assert big > 0          # the fixup path ran
+
+
 def test_sift_matches_oracle():
     from oracle import _olib as O
     from monocular_visual_odometry_va4mr_amd import cv2compat as G
