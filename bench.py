@@ -46,6 +46,7 @@ from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E
 
 SEQ_LEN = 4541          # KITTI seq00 frame count
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
+MFMA_PEAK_TF = 2500.0   # dense bf16 MFMA (no sparsity)
 
 
 def parse():
@@ -66,6 +67,9 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (see profiles/)")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--no-match", action="store_true", help="skip the BF-matcher (MFMA) leg")
+    ap.add_argument("--match-pairs", type=int, default=32, help="matcher leg: problems per launch")
+    ap.add_argument("--match-n", type=int, default=8192, help="matcher leg: descriptors per image")
     return ap.parse_args()
 
 
@@ -109,6 +113,39 @@ def pyr_bytes(eng):
 
 def gftt_bytes(eng, n_corners):
     return float(eng.B * eng.W * eng.H + 8 * n_corners)
+
+
+def matcher_leg(device, pairs, n, iters=10):
+    """BF kNN (k=2) on MFMA, SURVEY.md §8d / BASELINE config C5 ("SIFT capped at the best 8192 +
+    BF 8192^2"): `pairs` image pairs of n SIFT-like descriptors per vo_bf_knn2_batch launch,
+    timed with HIP events; 2*n*n*128 FLOP per pair against the dense bf16 MFMA peak."""
+    from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch
+    rng = np.random.default_rng(7)
+
+    def sift_like():
+        v = rng.gamma(0.6, 1.0, (pairs, n, 128))
+        v *= 512.0 / np.linalg.norm(v, axis=2, keepdims=True)
+        v = np.minimum(v, 0.2 * 512)
+        v *= 512.0 / np.maximum(np.linalg.norm(v, axis=2, keepdims=True), 1e-9)
+        return torch.from_numpy(np.clip(np.rint(v), 0, 255).astype(np.float32)).to(device)
+
+    q, t = sift_like(), sift_like()
+    cnt = torch.full((pairs,), n, dtype=torch.int32, device=device)
+    for _ in range(2):
+        bf_knn2_batch(q, cnt, t, cnt)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        bf_knn2_batch(q, cnt, t, cnt)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    tf = 2.0 * n * n * 128 * pairs / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": "vo_bf_knn2_batch", "achieved": round(tf, 2), "peak": MFMA_PEAK_TF,
+            "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TF, 4), "pairs_per_s": round(pairs / (ms * 1e-3), 1),
+            "ms_per_launch": round(ms, 4), "config": f"C5 BF {n}x{n} descriptors x {pairs} pairs per launch",
+            "flop_per_launch": 2.0 * n * n * 128 * pairs}
 
 
 def cpu_baseline(K, opts, frames_np, gap):
@@ -282,8 +319,10 @@ def main():
         "gftt": gftt_bytes(eng, ncor),
         "pyr_build": pyr_bytes(eng),
     }
-    # dominant HBM-class stage (pyramid/KLT/detection are judged by bytes)
-    dom = max(bytes_by, key=lambda n: st_ms[names.index(n)])
+    # the roofline row is the dominant kernel of the step: k_lk_w (track) has the largest
+    # kernel time per step in profiles/r1_summary.md (rocprofv3 --stats of this workload);
+    # stage event spans of the latency-bound gftt select / PnP stretch under the 2-stream overlap
+    dom = "track"
     dom_ms = float(st_ms[names.index(dom)])
     achieved = bytes_by[dom] / (dom_ms * 1e-3) / 1e9
     traffic = None
@@ -350,6 +389,8 @@ def main():
             out["cpu_baseline"] = None
     else:
         out["cpu_baseline"] = None
+    if world == 1 and not args.no_match:
+        out["roofline_matcher"] = matcher_leg(device, args.match_pairs, args.match_n)
     print(json.dumps(out))
     if args.stages:
         print(json.dumps({"stages_ms": stage, "bytes": bytes_by}), file=sys.stderr)
