@@ -11,6 +11,8 @@
 // so distances are exact; the per-query top-2 scan keeps OpenCV's tie order.
 #include "vo_dev.h"
 
+#include <stdlib.h>
+
 #include <float.h>
 #include <limits.h>
 #include <math.h>
@@ -511,6 +513,175 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
     }
 }
 
+// k_sift_desc_w: calcSIFTDescriptor with one WAVE per keypoint and the same arithmetic, in
+// the same order, as k_sift_desc (and the C restatement).
+//  * window positions are processed 64 at a time in raster order: each lane computes one
+//    position's gradient, weight, bins and its eight trilinear contributions (the per-pixel
+//    math, in parallel); the valid ones are compacted into LDS in raster order;
+//  * the histogram (360 bins) is owned by lanes: bin b lives in lane b % 64, register b / 64.
+//    The eight bins a pixel touches (idx + {0, 1, 10, 11, 60, 61, 70, 71}) fall in eight
+//    distinct lanes, so every lane walks the chunk's valid pixels in order and adds the one
+//    contribution that lands in its bins (0 elsewhere, which leaves a register unchanged):
+//    each bin receives its additions in exactly the serial order;
+//  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
+#define SIFT_HITMASK ((1ull << 0) | (1ull << 1) | (1ull << 6) | (1ull << 7) | (1ull << 10) | (1ull << 11) | \
+                      (1ull << 60) | (1ull << 61))
+__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
+{
+    __shared__ int pidx_s[4][64];
+    __shared__ float pval_s[4][64 * 8];
+    __shared__ float hist_s[4][384];
+    __shared__ float dst_s[4][128];
+    __shared__ float red_s[4][2];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + w;
+    if (q >= sb.counters[2]) return;
+    int* pidx = pidx_s[w];
+    float* pval = pval_s[w];
+    float* hist = hist_s[w];
+    float* dsl = dst_s[w];
+    const float* tab = sb.consts + EXPTAB_OFF;
+    const float* kp = sb.kp_out + 6 * (int64_t)q;
+    const int kpo = (int)kp[5];
+    int octave = kpo & 255, layer = (kpo >> 8) & 255;
+    octave = octave < 128 ? octave : (-128 | octave);
+    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+    const float size = kp[2] * scale;
+    const float ptx = kp[0] * scale, pty = kp[1] * scale;
+    const int oi = octave + 1;
+    const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
+    const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
+    float angle = 360.f - kp[3];
+    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+    const float ori = angle, scl = size * 0.5f;
+    const int d = 4, n = 8;
+    const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
+    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180)));
+    float sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    const float bins_per_rad = n / 360.f;
+    const float exp_scale = -1.f / (d * d * 0.5f);
+    const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
+    int radius = __float2int_rn(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+    const int rmax = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
+    if (radius > rmax) radius = rmax;
+    cos_t /= hist_width;
+    sin_t /= hist_width;
+    const int side = 2 * radius + 1;
+    const int total = side * side;
+    float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, h4 = 0.f, h5 = 0.f;
+    for (int base = 0; base < total; base += 64) {
+        const int pos = base + lane;
+        bool valid = false;
+        int idx = 0;
+        float vv[8];
+        if (pos < total) {
+            const int ii = pos / side;
+            const int i = ii - radius, j = pos - ii * side - radius;
+            const float c_rot = j * cos_t - i * sin_t;
+            const float r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + d / 2 - 0.5f;
+            float cbin = c_rot + d / 2 - 0.5f;
+            const int r = ptiy + i, c = ptix + j;
+            valid = rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+            if (valid) {
+                const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
+                const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
+                const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
+                const float o = fast_atan2(dy, dx);
+                const float mag = sqrtf(dx * dx + dy * dy) * wgt;
+                float obin = (o - ori) * bins_per_rad;
+                int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
+                rbin -= r0; cbin -= c0; obin -= o0;
+                if (o0 < 0) o0 += n;
+                if (o0 >= n) o0 -= n;
+                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+                // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
+                vv[0] = v_rco000; vv[1] = v_rco001; vv[2] = v_rco010; vv[3] = v_rco011;
+                vv[4] = v_rco100; vv[5] = v_rco101; vv[6] = v_rco110; vv[7] = v_rco111;
+            }
+        }
+        const uint64_t m = __ballot(valid);
+        const int nv = __popcll(m);
+        if (valid) {
+            const int slot = __popcll(m & ((1ull << lane) - 1ull));
+            pidx[slot] = idx;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pval[slot * 8 + k] = vv[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int p = 0; p < nv; ++p) {
+            const int id = pidx[p];
+            const int off = (lane - id) & 63;
+            const bool hit = (SIFT_HITMASK >> off) & 1ull;
+            // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
+            const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
+            const float v = hit ? pval[p * 8 + sl] : 0.f;
+            const int real = off + (off == 6 || off == 7 ? 64 : 0);
+            const int k = (id + real - lane) >> 6;
+            h0 += k == 0 ? v : 0.f;
+            h1 += k == 1 ? v : 0.f;
+            h2 += k == 2 ? v : 0.f;
+            h3 += k == 3 ? v : 0.f;
+            h4 += k == 4 ? v : 0.f;
+            h5 += k == 5 ? v : 0.f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    hist[lane] = h0; hist[lane + 64] = h1; hist[lane + 128] = h2;
+    hist[lane + 192] = h3; hist[lane + 256] = h4; hist[lane + 320] = h5;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // circular orientation wrap + copy (independent per output)
+    for (int t = lane; t < d * d * n; t += 64) {
+        const int cell = t / n, k = t - cell * n;
+        const int i = cell / d, j = cell - i * d;
+        const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+        float v = hist[idx + k];
+        if (k < 2) v += hist[idx + n + k];
+        dsl[t] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int len = d * d * n;
+    if (lane == 0) {
+        float nrm2 = 0;
+        for (int k = 0; k < len; ++k) nrm2 += dsl[k] * dsl[k];
+        const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
+        nrm2 = 0;
+        for (int i = 0; i < len; ++i) {
+            const float v = dsl[i] < thr ? dsl[i] : thr;
+            nrm2 += v * v;
+        }
+        red_s[w][0] = thr;
+        red_s[w][1] = nrm2;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float thr = red_s[w][0];
+    const float s2 = sqrtf(red_s[w][1]);
+    const float nscale = SIFT_INT_DESCR_FCTR / (s2 > FLT_EPSILON ? s2 : FLT_EPSILON);
+    float* dst = sb.desc + 128 * (int64_t)q;
+    for (int t = lane; t < len; t += 64) {
+        const float v = dsl[t] < thr ? dsl[t] : thr;
+        const int iv = __float2int_rn(v * nscale);
+        dst[t] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
+    }
+}
+
 // ------------------------------------------------------- brute-force kNN (k = 2)
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -753,7 +924,13 @@ extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, 
     }
     hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
     hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1), dim3(1024), 0, st, *sb);
-    hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64), dim3(64), 0, st, *sb);
+    // wave-per-keypoint descriptor kernel unless VO_SIFT_DESC_SERIAL=1 (thread per keypoint;
+    // both produce identical descriptors)
+    const char* ser = getenv("VO_SIFT_DESC_SERIAL");
+    if (ser && atoi(ser) == 1)
+        hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64), dim3(64), 0, st, *sb);
+    else
+        hipLaunchKernelGGL(k_sift_desc_w, dim3((sb->kp_cap + 3) / 4), dim3(256), 0, st, *sb);
     return hip_rc();
 }
 

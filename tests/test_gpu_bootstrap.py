@@ -89,6 +89,26 @@ def test_sift_matches_oracle():
     assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
 
 
+def test_sift_desc_wave_equals_serial(monkeypatch):
+    """The wave-per-keypoint descriptor kernel reproduces the thread-per-keypoint one bit for
+    bit (same per-bin accumulation order), on KITTI- and Malaga-size frames."""
+    from monocular_visual_odometry_va4mr_amd.features import Sift
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    for preset, seed in (("kitti", 1), ("malaga1024", 2)):
+        fr, _, _, _ = make_sequence(preset, 1, seed=seed)
+        img = torch.from_numpy(np.ascontiguousarray(fr[0])).cuda()
+        sift = Sift(img.shape[1], img.shape[0], "cuda")
+        out = {}
+        for mode in ("1", "0"):
+            monkeypatch.setenv("VO_SIFT_DESC_SERIAL", mode)
+            sift.run(img)
+            kp, desc = sift.result()
+            out[mode] = (kp.copy(), desc.copy())
+        assert len(out["0"][0]) > 500
+        assert np.array_equal(out["0"][0], out["1"][0])
+        assert np.array_equal(out["0"][1], out["1"][1]), f"{preset}: descriptors differ"
+
+
 def test_essential_and_recover_pose():
     from oracle import _olib as O
     from monocular_visual_odometry_va4mr_amd import cv2compat as G

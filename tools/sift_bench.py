@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""SIFT detectAndCompute time per image (vo_sift) on KITTI / Malaga-1024 / 1080p synthetic
+frames, thread-per-keypoint vs wave-per-keypoint descriptor kernel (VO_SIFT_DESC_SERIAL),
+plus one SIFT+SIFT+BF-match pair (BASELINE config C3).  Prints one JSON line per size."""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from monocular_visual_odometry_va4mr_amd.features import Sift, bf_knn2  # noqa: E402
+from monocular_visual_odometry_va4mr_amd.synth import make_sequence  # noqa: E402
+
+
+def timed(fn, iters):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    for preset in ("kitti", "malaga1024", "hd1080"):
+        fr, _, _, _ = make_sequence(preset, 2, seed=2)
+        a = torch.from_numpy(np.ascontiguousarray(fr[0])).cuda()
+        b = torch.from_numpy(np.ascontiguousarray(fr[1])).cuda()
+        s0 = Sift(a.shape[1], a.shape[0], "cuda")
+        s1 = Sift(a.shape[1], a.shape[0], "cuda")
+        res = {"preset": preset, "W": a.shape[1], "H": a.shape[0]}
+        for mode in ("1", "0"):
+            os.environ["VO_SIFT_DESC_SERIAL"] = mode
+            res["ms_per_image_" + ("serial_desc" if mode == "1" else "wave_desc")] = round(timed(lambda: s0.run(a), iters), 3)
+        s0.run(a)
+        s1.run(b)
+        torch.cuda.synchronize()
+        res["keypoints"] = int(s0.t["counters"][2])
+
+        def pair():
+            k0, d0, n0 = s0.run(a)
+            k1, d1, n1 = s1.run(b)
+            bf_knn2(d0, n0, d1, n1, d0.shape[0])
+
+        res["ms_per_pair_sift_sift_match"] = round(timed(pair, iters), 3)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
