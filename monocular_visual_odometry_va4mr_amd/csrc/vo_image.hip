@@ -302,9 +302,6 @@ VO_DEV __amdgpu_buffer_rsrc_t lkq_rsrc(const void* base, int64_t bytes)
 #ifndef LK_JPRE
 #define LK_JPRE 1
 #endif
-#ifndef LK_QTC
-#define LK_QTC 3            // QT build: LDS reads batched over this many trips
-#endif
 VO_DEV void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -568,11 +565,13 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
     constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
-    __shared__ uint32_t QT[TH * TW];
+    constexpr int QM = (TW + 3) / 4, QS = 4 * QM;      // QT: quads of 4 columns, row stride QS
+    static_assert(JRW >= QM + 1, "J rows must cover the quad groups");
+    __shared__ uint4 QT4[TH * QM];
+    const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
     __shared__ uint32_t JR[(TH + 1) * JRW];
     __shared__ uint32_t IR[(WH + 1) * IRW];
     __shared__ uint32_t DR[(WH + 1) * DRW];
-    const uint8_t* jr8 = (const uint8_t*)JR;
     const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb, pcur = -1;
     const int lane = lane_id();
@@ -596,7 +595,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     for (int j = 0; j < MAXJ; ++j) {
         const int k = lane + 64 * j;
         live[j] = k < NPX;
-        toff[j] = live[j] ? (k / WW) * TW + k % WW : 0;
+        toff[j] = live[j] ? (k / WW) * QS + k % WW : 0;
     }
     int tx0 = 0, ty0 = 0, jsh = 0;
     int cols = 0, rows = 0, pitch = 0, loff = 0;
@@ -608,7 +607,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     // and store (LDS writes), so that every load of a stage is in flight at once: one memory
     // round trip per stage instead of one per loop trip.
     constexpr int NIR = ((WH + 1) * IRW + 63) / 64, NDR = ((WH + 1) * DRW + 63) / 64;
-    constexpr int NJR = ((TH + 1) * JRW + 63) / 64, NQT = (TH * TW + 63) / 64;
+    constexpr int NJR = ((TH + 1) * JRW + 63) / 64, NQT = (TH * QM + 63) / 64;
     // J tile origin covering the window at (inx, iny)
     auto j_origin = [&](int inx, int iny) {
         tx0 = max(inx - LK_M, -VO_BORDER);
@@ -631,7 +630,9 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
             }
         }
     };
-    // JR rows -> LDS, then the packed 2x2 quads QT (LDS -> LDS, reads batched 3 trips at a time)
+    // JR rows -> LDS, then the packed 2x2 quads QT: one item = row r, columns 4m..4m+3, built
+    // from four aligned JR dwords with byte-align and two rounds of byte permutes and stored as
+    // one 16-B write; quad byte order (J[r][c], J[r][c+1], J[r+1][c], J[r+1][c+1])
     auto j_store = [&](const uint32_t (&v)[NJR]) {
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
@@ -639,24 +640,22 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
             if (q < (TH + 1) * JRW) JR[q] = v[k];
         }
         wave_lds_sync();
+        const int ln = lane + opaque0();
 #pragma unroll
-        for (int k0 = 0; k0 < NQT; k0 += LK_QTC) {
-            uint32_t t0[LK_QTC], t1[LK_QTC], t2[LK_QTC], t3[LK_QTC];
-            const int ln = lane + opaque0();
-#pragma unroll
-            for (int i = 0; i < LK_QTC; ++i) {
-                const int q = ln + 64 * (k0 + i);
-                t0[i] = t1[i] = t2[i] = t3[i] = 0u;
-                if (k0 + i < NQT && q < TH * TW) {
-                    const int r = q / TW, c = q - r * TW;
-                    const uint8_t* s = jr8 + r * (4 * JRW) + jsh + c;
-                    t0[i] = s[0]; t1[i] = s[1]; t2[i] = s[4 * JRW]; t3[i] = s[4 * JRW + 1];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < LK_QTC; ++i) {
-                const int q = lane + 64 * (k0 + i);
-                if (k0 + i < NQT && q < TH * TW) QT[q] = t0[i] | (t1[i] << 8) | (t2[i] << 16) | (t3[i] << 24);
+        for (int k = 0; k < NQT; ++k) {
+            const int q = ln + 64 * k;
+            if (q < TH * QM) {
+                const int r = q / QM, m = q - r * QM;
+                const uint32_t* j0 = JR + r * JRW + m;
+                const uint32_t a0 = j0[0], a1 = j0[1], b0 = j0[JRW], b1 = j0[JRW + 1];
+                const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
+                const uint32_t Bv = jsh == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, jsh + 1);
+                const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
+                const uint32_t D = jsh == 3 ? b1 : __builtin_amdgcn_alignbyte(b1, b0, jsh + 1);
+                const uint32_t X = __builtin_amdgcn_perm(Bv, A, 0x05010400u), Y = __builtin_amdgcn_perm(Bv, A, 0x07030602u);
+                const uint32_t Xp = __builtin_amdgcn_perm(D, C, 0x05010400u), Yp = __builtin_amdgcn_perm(D, C, 0x07030602u);
+                QT4[q] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
+                                    __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
             }
         }
         wave_lds_sync();
@@ -831,7 +830,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     const int neg = w11 < 0;
                     const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
                     const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
-                    const uint32_t* tb = QT + (iny - ty0) * TW + (inx - tx0);
+                    const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int b1 = 0, b2 = 0;
 #pragma unroll
                     for (int j = 0; j < MAXJ; ++j) {
@@ -886,7 +885,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     const int neg = w11 < 0;
                     const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
                     const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
-                    const uint32_t* tb = QT + (iny - ty0) * TW + (inx - tx0);
+                    const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int es = 0;
 #pragma unroll
                     for (int j = 0; j < MAXJ; ++j) {
