@@ -560,18 +560,23 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
 template <int WW, int WH>
-__global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
 {
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
     constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
     constexpr int QM = (TW + 3) / 4, QS = 4 * QM;      // QT: quads of 4 columns, row stride QS
-    static_assert(JRW >= QM + 1, "J rows must cover the quad groups");
+    // LDS rows: QT quads, the I window bytes and the dI dwords all have the row stride QS (in
+    // their element), so one per-lane offset toff = row * QS + col indexes all three; JR rows
+    // are 8 dwords, so the staging lane -> (row, dword) map is (lane / 8, lane % 8)
+    constexpr int IRS = QS / 4, JRS = 8;
+    static_assert(JRW >= QM + 1 && JRW <= JRS && IRW <= IRS && IRW <= 8 && DRW == 16 && QS % 4 == 0,
+                  "k_lk_w staging layout");
     __shared__ uint4 QT4[TH * QM];
     const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
-    __shared__ uint32_t JR[(TH + 1) * JRW];
-    __shared__ uint32_t IR[(WH + 1) * IRW];
-    __shared__ uint32_t DR[(WH + 1) * DRW];
+    __shared__ uint32_t JR[(TH + 1) * JRS];
+    __shared__ uint32_t IR[(WH + 1) * IRS];
+    __shared__ uint32_t DR[(WH + 1) * QS];
     const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb, pcur = -1;
     const int lane = lane_id();
@@ -606,8 +611,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     // Staging is split into issue (global loads into registers, fixed unrolled trip counts)
     // and store (LDS writes), so that every load of a stage is in flight at once: one memory
     // round trip per stage instead of one per loop trip.
-    constexpr int NIR = ((WH + 1) * IRW + 63) / 64, NDR = ((WH + 1) * DRW + 63) / 64;
-    constexpr int NJR = ((TH + 1) * JRW + 63) / 64, NQT = (TH * QM + 63) / 64;
+    constexpr int NIR = ((WH + 1) * 8 + 63) / 64, NDR = ((WH + 1) * 16 + 63) / 64;
+    constexpr int NJR = ((TH + 1) * JRS + 63) / 64, NQT = (TH * QM + 63) / 64;
     // J tile origin covering the window at (inx, iny)
     auto j_origin = [&](int inx, int iny) {
         tx0 = max(inx - LK_M, -VO_BORDER);
@@ -616,17 +621,14 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
     };
     auto j_issue = [&](uint32_t (&v)[NJR]) {
         const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
-        const int base = loff + gy0 * pitch + (gx0 & ~3);          // wave-uniform
         const int ln = lane + opaque0();
+        const int vo = loff + gy0 * pitch + (gx0 & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
-            const int q = ln + 64 * k;
             v[k] = 0u;
-            if (q < (TH + 1) * JRW) {
-                const int r = q / JRW, c = q - r * JRW;
-                const int o = r * pitch + 4 * c;
-                LKCHKO(base + o, P.pstride, "J");
-                v[k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, o, base, 0);
+            if ((lane >> 3) + 8 * k < TH + 1) {
+                LKCHKO(vo + 8 * k * pitch, P.pstride, "J");
+                v[k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, vo, 8 * k * pitch, 0);
             }
         }
     };
@@ -637,7 +639,7 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
             const int q = lane + 64 * k;
-            if (q < (TH + 1) * JRW) JR[q] = v[k];
+            if (q < (TH + 1) * JRS) JR[q] = v[k];
         }
         wave_lds_sync();
         const int ln = lane + opaque0();
@@ -646,8 +648,8 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
             const int q = ln + 64 * k;
             if (q < TH * QM) {
                 const int r = q / QM, m = q - r * QM;
-                const uint32_t* j0 = JR + r * JRW + m;
-                const uint32_t a0 = j0[0], a1 = j0[1], b0 = j0[JRW], b1 = j0[JRW + 1];
+                const uint32_t* j0 = JR + r * JRS + m;
+                const uint32_t a0 = j0[0], a1 = j0[1], b0 = j0[JRS], b1 = j0[JRS + 1];
                 const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
                 const uint32_t Bv = jsh == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, jsh + 1);
                 const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
@@ -718,32 +720,20 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 LKPROF_T(ti0);
                 const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
                 const int ish = gx & 3;
-                const int ibase = loff + gy * pitch + (gx & ~3);           // wave-uniform byte offsets
-                const int dbase = 2 * (loff + gy * pitch + gx);             // dx plane; dy at +2 * dplane
-                uint32_t vir[NIR], vdx[NDR], vdy[NDR], vjr[NJR];
                 const int ln = lane + opaque0();
+                const int vi = loff + gy * pitch + (gx & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);   // 8 dwords / row
+                const int vd = 2 * (loff + gy * pitch + gx + (ln >> 4) * pitch + (ln & 15));    // 16 int16 / row
+                uint32_t vir[NIR], vdx[NDR], vdy[NDR], vjr[NJR];
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
-                    const int q = ln + 64 * k;
-                    vir[k] = 0u;
-                    if (q < (WH + 1) * IRW) {
-                        const int r = q / IRW, c = q - r * IRW;
-                        const int o = r * pitch + 4 * c;
-                        LKCHKO(ibase + o, P.pstride, "I");
-                        vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, o, ibase, 0);
-                    }
+                    LKCHKO(vi + 8 * k * pitch, P.pstride, "I");
+                    vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, vi, 8 * k * pitch, 0);
                 }
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
-                    const int q = ln + 64 * k;
-                    vdx[k] = vdy[k] = 0u;
-                    if (q < (WH + 1) * DRW) {
-                        const int r = q / DRW, c = q - r * DRW;
-                        const int o = 2 * (r * pitch + c);
-                        LKCHKO(dbase + o, 2 * P.dplane, "Dx");
-                        vdx[k] = __builtin_amdgcn_raw_buffer_load_b16(rDX, o, dbase, 0);
-                        vdy[k] = __builtin_amdgcn_raw_buffer_load_b16(rDY, o, dbase, 0);
-                    }
+                    LKCHKO(vd + 8 * k * pitch, 2 * P.dplane, "Dx");
+                    vdx[k] = __builtin_amdgcn_raw_buffer_load_b16(rDX, vd, 8 * k * pitch, 0);
+                    vdy[k] = __builtin_amdgcn_raw_buffer_load_b16(rDY, vd, 8 * k * pitch, 0);
                 }
                 {
                     const int jx = (int)floorf(ox - hx), jy = (int)floorf(oy - hy);
@@ -757,13 +747,13 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 wave_lds_sync();
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
-                    const int q = lane + 64 * k;
-                    if (q < (WH + 1) * IRW) IR[q] = vir[k];
+                    const int r = (ln >> 3) + 8 * k, c = ln & 7;
+                    if (c < IRS) IR[r * IRS + c] = vir[k];
                 }
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
-                    const int q = lane + 64 * k;
-                    if (q < (WH + 1) * DRW) DR[q] = vdx[k] | (vdy[k] << 16);
+                    const int r = (ln >> 4) + 4 * k, c = ln & 15;
+                    DR[r * QS + c] = vdx[k] | (vdy[k] << 16);
                 }
                 if (staged) j_store(vjr);      // syncs
                 else wave_lds_sync();
@@ -778,13 +768,11 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                 int a11 = 0, a12 = 0, a22 = 0;
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
-                    const int kk = lane + opaque0() + 64 * j;
-                    const int wy = live[j] ? kk / WW : 0, wx = live[j] ? kk - (kk / WW) * WW : 0;
-                    const uint8_t* s = ir8 + wy * (4 * IRW) + ish + wx;
-                    const uint32_t* d = DR + wy * DRW + wx;
-                    const uint32_t d00 = d[0], d01 = d[1], d10 = d[DRW], d11 = d[DRW + 1];
+                    const uint8_t* s = ir8 + toff[j] + ish;
+                    const uint32_t* d = DR + toff[j];
+                    const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
                     const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
-                                          __mul24((int)s[4 * IRW], iw10) + __mul24((int)s[4 * IRW + 1], iw11), 9);
+                                          __mul24((int)s[QS], iw10) + __mul24((int)s[QS + 1], iw11), 9);
                     const int gx2 = DESCALE(__mul24((int)(int16_t)d00, iw00) + __mul24((int)(int16_t)d01, iw01) +
                                             __mul24((int)(int16_t)d10, iw10) + __mul24((int)(int16_t)d11, iw11), 14);
                     const int gy2 = DESCALE(__mul24((int)(int16_t)(d00 >> 16), iw00) + __mul24((int)(int16_t)(d01 >> 16), iw01) +
@@ -796,7 +784,12 @@ __global__ void __launch_bounds__(64) k_lk_w(LKParams P, int level_hi, int level
                     a12 += __mul24(ixv[j], iyv[j]);
                     a22 += __mul24(iyv[j], iyv[j]);
                 }
-                const int64_t iA11 = wave_sum_split(a11), iA12 = wave_sum_split(a12), iA22 = wave_sum_split(a22);
+                // one exact 32-bit reduction each unless a lane's partial could overflow the sum
+                const bool twide = __ballot((uint32_t)a11 >= (1u << 25) || (uint32_t)a22 >= (1u << 25) ||
+                                            (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
+                int64_t iA11, iA12, iA22;
+                if (!twide) { iA11 = wave_sum_dpp(a11); iA12 = wave_sum_dpp(a12); iA22 = wave_sum_dpp(a22); }
+                else { iA11 = wave_sum_split(a11); iA12 = wave_sum_split(a12); iA22 = wave_sum_split(a22); }
                 const float FLT_SCALE = 1.f / (1 << 20);
                 const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
                 float D = A11 * A22 - A12 * A12;
