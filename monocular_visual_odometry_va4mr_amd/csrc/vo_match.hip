@@ -8,12 +8,13 @@
 //  k_bf_prep   descriptors -> bf16 rows + integer squared norms (one wave per row)
 //  k_bf_mfma   block = 4 waves x 32 queries; 64-row train tiles double-buffered in LDS (16-B
 //              slots XOR-swizzled by row: conflict-free ds_read_b128); per 32-row sub-tile each
-//              wave runs 8 v_mfma_f32_32x32x16_bf16 with the TRAIN rows as the A operand and its
-//              queries as B, so every lane owns one query column and 16 train rows of the tile.
-//              The lane keeps a running top-2 of d' = |t|^2 - 2 q.t (the query's |q|^2 is a
-//              constant per lane and is added at the end) with strict '<' in increasing train
-//              index, i.e. the (distance, index) order OpenCV's knnMatch produces; a per-lane
-//              min over the 16 candidates skips the insertion when none can enter.
+//              wave runs 9 v_mfma_f32_32x32x16_bf16 with the TRAIN rows as the A operand and its
+//              queries as B, so every lane owns one query column and 16 train rows of the tile;
+//              the ninth K-step folds |t|^2 in, so the accumulator is s = 2 q.t - |t|^2 exactly.
+//              The lane keeps a running top-2 of s (= |q|^2 - d^2, |q|^2 constant per lane) with
+//              strict '>' in increasing train index, i.e. the (distance, index) order OpenCV's
+//              knnMatch produces; a per-lane max over the 16 candidates skips the insertion
+//              when none can enter.
 //  k_bf_merge  merges the train splits (grid filling for small batches) and writes
 //              idx2 / dist2 = sqrtf(d2) (correctly rounded, as OpenCV's sqrt).
 //  k_bf_fixup  integer order equals float order only while sqrtf separates the integers
@@ -66,9 +67,10 @@ VO_DEV void merge2(int& d0, int& i0, int& d1, int& i1, int e0, int j0, int e1, i
     d0 = r0; i0 = s0; d1 = r1; i1 = s1;
 }
 
-// descriptors -> bf16 + |v|^2; rows >= n untouched (never read)
+// descriptors -> bf16 (times `mul`: 2 for queries, 1 for train rows; exact for integers
+// 0..255) + |v|^2; rows >= n untouched (never read)
 __global__ void __launch_bounds__(256) k_bf_prep(const float* __restrict__ src, const int32_t* n, int B, int cap,
-                                                 __bf16* __restrict__ dst, int32_t* __restrict__ nrm)
+                                                 float mul, __bf16* __restrict__ dst, int32_t* __restrict__ nrm)
 {
     const int row = blockIdx.x * 4 + wave_id();
     const int b = row / cap, r = row - b * cap;
@@ -77,16 +79,23 @@ __global__ void __launch_bounds__(256) k_bf_prep(const float* __restrict__ src, 
     const float2 v = *reinterpret_cast<const float2*>(src + (int64_t)row * 128 + 2 * lane);
     const int a = (int)v.x, c = (int)v.y;
     __bf16* o = dst + (int64_t)row * 128 + 2 * lane;
-    o[0] = (__bf16)v.x;
-    o[1] = (__bf16)v.y;
+    o[0] = (__bf16)(v.x * mul);
+    o[1] = (__bf16)(v.y * mul);
     const int s = wave_sum_dpp(a * a + c * c);
     if (lane == 0) nrm[row] = s;
 }
 
+// The |t|^2 term rides in the MFMA as a ninth K-step: train row t carries its norm split into
+// bytes (tn = a * 65536 + b * 256 + c) in K columns 128..130 and every query carries
+// (-65536, -256, -1) there, while the queries' descriptor columns hold 2q.  The accumulator is
+// then exactly s = 2 q.t - |t|^2 = |q|^2 - d^2 (every partial sum is an integer below 2^24),
+// and the top-2 is a running maximum of s.  Absent train rows carry a = 255 (s < -2^24 + ...),
+// below BF_FLOOR, which no real row reaches (s >= -|t|^2 >= -128 * 255^2).
+#define BF_FLOOR (-16500000.f)
 __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 {
     __shared__ uint4 tile[2][BF_TT * 16];
-    __shared__ int4 tnl[2][BF_TT / 4];
+    __shared__ uint4 tnp[2][BF_TT * 2];          // norm bytes (k = 128..135) | zeros (136..143)
     const int nqb = (A.qcap + BF_QB - 1) / BF_QB;
     int blk = blockIdx.x;
     const int sp = blk % A.tsplit;
@@ -109,10 +118,12 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 #pragma unroll
         for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s);
     }
+    bf16x8 qn9 = {};                              // K columns 128..135 / 136..143 of every query
+    if (h == 0) { qn9[0] = (__bf16)(-65536.f); qn9[1] = (__bf16)(-256.f); qn9[2] = (__bf16)(-1.f); }
     const uint4* Tg = reinterpret_cast<const uint4*>(A.tbf + (int64_t)b * A.tcap * 128);
     const int32_t* TN = A.tn + (int64_t)b * A.tcap;
     uint4 pre[4];
-    int pren = INT_MAX;
+    int pren = 255 << 16;
     auto gload = [&](int t0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -120,7 +131,7 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
             const int r = t0 + row;
             pre[i] = r < thi ? Tg[(int64_t)r * 16 + slot] : make_uint4(0u, 0u, 0u, 0u);
         }
-        pren = (tid < BF_TT && t0 + tid < thi) ? TN[t0 + tid] : INT_MAX;
+        pren = (tid < BF_TT && t0 + tid < thi) ? TN[t0 + tid] : (255 << 16);
     };
     auto lstore = [&](int buf) {
 #pragma unroll
@@ -128,9 +139,17 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
             const int g = tid + 256 * i, row = g >> 4, slot = g & 15;
             tile[buf][row * 16 + (slot ^ (row & 15))] = pre[i];
         }
-        if (tid < BF_TT) reinterpret_cast<int*>(tnl[buf])[tid] = pren;
+        if (tid < BF_TT) {
+            bf16x8 nb = {};
+            nb[0] = (__bf16)(float)(pren >> 16);
+            nb[1] = (__bf16)(float)((pren >> 8) & 255);
+            nb[2] = (__bf16)(float)(pren & 255);
+            tnp[buf][2 * tid] = *reinterpret_cast<const uint4*>(&nb);
+            tnp[buf][2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
+        }
     };
-    int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
+    float s0 = BF_FLOOR, s1 = BF_FLOOR;
+    int i0 = -1, i1 = -1;
     if (ntile > 0) {
         gload(tlo);
         lstore(0);
@@ -148,30 +167,26 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
                 const bf16x8 af = *reinterpret_cast<const bf16x8*>(&tile[buf][row * 16 + ((2 * s + h) ^ (row & 15))]);
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qf[s], acc, 0, 0, 0);
             }
-            // C layout: column = lane & 31 (query), row = (reg & 3) + 8 * (reg >> 2) + 4 * h (train)
-            int dv[16];
-            int m = INT_MAX;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int4 tv = tnl[buf][(sub * 32 + 8 * g + 4 * h) >> 2];
-                const int tt[4] = {tv.x, tv.y, tv.z, tv.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int reg = 4 * g + e;
-                    dv[reg] = tt[e] == INT_MAX ? INT_MAX : tt[e] - 2 * (int)acc[reg];
-                    m = min(m, dv[reg]);
-                }
+            {
+                const bf16x8 af = *reinterpret_cast<const bf16x8*>(&tnp[buf][2 * row + h]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qn9, acc, 0, 0, 0);
             }
-            if (m < d1) {
+            // C layout: column = lane & 31 (query), row = (reg & 3) + 8 * (reg >> 2) + 4 * h (train)
+            float m = acc[0];
+#pragma unroll
+            for (int reg = 1; reg < 16; ++reg) m = fmaxf(m, acc[reg]);
+            if (m > s1) {
                 const int ib = t0 + sub * 32 + 4 * h;
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
-                    const int d = dv[reg], ix = ib + (reg & 3) + 8 * (reg >> 2);
-                    const bool c0 = d < d0, c1 = d < d1;
-                    const int nd1 = c0 ? d0 : (c1 ? d : d1), ni1 = c0 ? i0 : (c1 ? ix : i1);
-                    d0 = c0 ? d : d0;
+                    const float v = acc[reg];
+                    const int ix = ib + (reg & 3) + 8 * (reg >> 2);
+                    const bool c0 = v > s0, c1 = v > s1;
+                    const float ns1 = c0 ? s0 : (c1 ? v : s1);
+                    const int ni1 = c0 ? i0 : (c1 ? ix : i1);
+                    s0 = c0 ? v : s0;
                     i0 = c0 ? ix : i0;
-                    d1 = nd1;
+                    s1 = ns1;
                     i1 = ni1;
                 }
             }
@@ -179,7 +194,8 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
         if (k + 1 < ntile) lstore(buf ^ 1);
         __syncthreads();
     }
-    // the two half-waves hold the same queries over different train rows
+    // d' = |t|^2 - 2 q.t = -s (absent: INT_MAX); the two half-waves hold the same queries
+    int d0 = i0 >= 0 ? -(int)s0 : INT_MAX, d1 = i1 >= 0 ? -(int)s1 : INT_MAX;
     merge2(d0, i0, d1, i1, __shfl_xor(d0, 32, 64), __shfl_xor(i0, 32, 64), __shfl_xor(d1, 32, 64),
            __shfl_xor(i1, 32, 64));
     if (h == 0 && qv) A.part[((int64_t)b * A.tsplit + sp) * A.qcap + qi] = make_int4(d0, i0, d1, i1);
@@ -298,9 +314,9 @@ extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_
     A.flag_list = (int32_t*)p;
     A.nq = nq; A.nt = nt; A.idx2 = idx2; A.dist2 = dist2;
     if (hipMemsetAsync(A.flag_n, 0, sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
-    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap,
+    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap, 2.f,
                        (__bf16*)A.qbf, (int32_t*)A.qn);
-    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * tcap + 3) / 4), dim3(256), 0, st, t, nt, B, tcap,
+    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * tcap + 3) / 4), dim3(256), 0, st, t, nt, B, tcap, 1.f,
                        (__bf16*)A.tbf, (int32_t*)A.tn);
     const int nqb = (qcap + BF_QB - 1) / BF_QB;
     hipLaunchKernelGGL(k_bf_mfma, dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
