@@ -180,14 +180,14 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const float v = acc[reg];
-                    const int ix = ib + (reg & 3) + 8 * (reg >> 2);
-                    const bool c0 = v > s0, c1 = v > s1;
-                    const float ns1 = c0 ? s0 : (c1 ? v : s1);
-                    const int ni1 = c0 ? i0 : (c1 ? ix : i1);
-                    s0 = c0 ? v : s0;
-                    i0 = c0 ? ix : i0;
-                    s1 = ns1;
-                    i1 = ni1;
+                    if (v > s1) {                       // rare: lanes whose candidate enters
+                        const int ix = ib + (reg & 3) + 8 * (reg >> 2);
+                        const bool c0 = v > s0;
+                        s1 = c0 ? s0 : v;
+                        i1 = c0 ? i0 : ix;
+                        s0 = c0 ? v : s0;
+                        i0 = c0 ? ix : i0;
+                    }
                 }
             }
         }
