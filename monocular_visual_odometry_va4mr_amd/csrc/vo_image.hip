@@ -54,15 +54,15 @@ struct PyrLevelArgs {
     int level;
 };
 
+// L0: level 0 (frame bytes; its instantiation carries no source-staging LDS, so more blocks
+// fit per CU)
+template <bool L0>
 __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
 {
     __shared__ uint32_t PVw[PV_H * PV_W / 4];
-    __shared__ uint32_t SRw[PS_H * PS_W / 4];
-    __shared__ uint16_t HS[PS_H * PV_W];
     __shared__ int yk[PV_H], xc[PV_W];
     __shared__ int mm[4];
     uint8_t* PV = (uint8_t*)PVw;
-    const uint8_t* SR = (const uint8_t*)SRw;
     const int tid = threadIdx.x;
     const int b = blockIdx.z;
     const int px0 = blockIdx.x * PT_W, py0 = blockIdx.y * PT_H;
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
     // every load of a phase is issued before the first one is consumed (fixed trip counts,
     // unrolled): the staging is latency-bound otherwise
     constexpr int NPV = (PV_H * PV_W + 255) / 256;
-    if (A.level == 0) {
+    if constexpr (L0) {
         const uint8_t* fr = A.src + (int64_t)b * A.sstride;
         uint32_t v[NPV];
 #pragma unroll
@@ -105,6 +105,9 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
             if (e < PV_H * PV_W) PV[e] = (uint8_t)v[i];
         }
     } else {
+        __shared__ uint32_t SRw[PS_H * PS_W / 4];
+        __shared__ uint16_t HS[PS_H * PV_W];
+        const uint8_t* SR = (const uint8_t*)SRw;
         // source rectangle (level l-1 coordinates) under the tile
         const int sy0 = 2 * mm[0] - 2, sy1 = 2 * mm[1] + 2;
         const int sx0 = 2 * mm[2] - 2, sx1 = 2 * mm[3] + 2;
@@ -1981,7 +1984,8 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
         const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
         if (A.pitch % 64 || A.pitch < pw) return VO_EARG;
         dim3 g((pw + PT_W - 1) / PT_W, (ph + PT_H - 1) / PT_H, d->B);
-        hipLaunchKernelGGL(k_pyr_level, g, dim3(256), 0, VO_STREAM(stream), A);
+        if (l == 0) hipLaunchKernelGGL(k_pyr_level<true>, g, dim3(256), 0, VO_STREAM(stream), A);
+        else hipLaunchKernelGGL(k_pyr_level<false>, g, dim3(256), 0, VO_STREAM(stream), A);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
 }
