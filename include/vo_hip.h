@@ -201,7 +201,7 @@ typedef struct vo_sift_buf {
     float* dog;                   /* difference of Gaussians                            */
     float* tmp;                   /* separable-blur scratch (2W*2H floats)              */
     float* consts;                /* [7*32 kernel taps][64 exp32f table] (host-filled)  */
-    int32_t* counters;            /* [4]: n_cand, n_kp, n_out, overflow                 */
+    int32_t* counters;            /* [8]: n_cand, n_kp, n_out, overflow, n_refined, -   */
     int32_t* cand;                /* extrema candidates [cand_cap][4] (o, layer, r, c)  */
     float* kp;                    /* raw keypoints [kp_cap][8]                          */
     float* kp_out;                /* sorted, deduplicated keypoints [kp_cap][6]         */

@@ -348,6 +348,150 @@ __global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
     }
 }
 
+// Two-stage form of k_sift_kp (default; VO_SIFT_KP_SERIAL=1 selects k_sift_kp):
+//  k_sift_refine  adjustLocalExtrema per candidate (one thread each) -> refined records in
+//                 the hist scratch (12 floats each), count in counters[4];
+//  k_sift_ori     calcOrientationHist + peak interpolation with one WAVE per refined keypoint:
+//                 lanes compute gradient / weight / bin of 64 window positions at a time (raster
+//                 order), the 36 bins are owned by lanes 0..35 and each lane adds, in pixel order,
+//                 the values that land in its bin -- the serial accumulation order, so the
+//                 histogram, its smoothing, the peaks and the emitted keypoints are identical.
+//                 (k_sift_kp's temphist[36] is indexed dynamically, i.e. lives in scratch.)
+//                 Keypoints are appended with atomics; k_sift_sort_dedupe orders them.
+#define SIFT_REC 12
+__global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nc = min(sb.counters[0], sb.cand_cap);
+    if (k >= nc) return;
+    const int o = sb.cand[4 * k], i0 = sb.cand[4 * k + 1];
+    int r1 = sb.cand[4 * k + 2], c1 = sb.cand[4 * k + 3], layer = i0;
+    KP kpt;
+    if (!adjust_local_extrema(sb, kpt, o, layer, r1, c1, 1.6f)) return;
+    const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
+    const int q = atomicAdd(&sb.counters[4], 1);
+    if (q >= rec_cap) { sb.counters[3] = 1; return; }
+    float* rec = sb.hist + (int64_t)SIFT_REC * q;
+    rec[0] = kpt.x; rec[1] = kpt.y; rec[2] = kpt.size; rec[3] = kpt.response;
+    rec[4] = __int_as_float(kpt.octave); rec[5] = __int_as_float(o); rec[6] = __int_as_float(layer);
+    rec[7] = __int_as_float(r1); rec[8] = __int_as_float(c1);
+}
+
+__global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
+{
+    __shared__ int4 pb_s4[4][16];
+    __shared__ float4 pv_s4[4][16];
+    __shared__ float th_s[4][SIFT_ORI_HIST_BINS + 4];
+    __shared__ float hs_s[4][SIFT_ORI_HIST_BINS];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + w;
+    const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
+    if (q >= min(sb.counters[4], rec_cap)) return;
+    int* pbin = reinterpret_cast<int*>(pb_s4[w]);
+    float* pval = reinterpret_cast<float*>(pv_s4[w]);
+    const float* rec = sb.hist + (int64_t)SIFT_REC * q;
+    const float kx = rec[0], ky = rec[1], ksize = rec[2], kresp = rec[3];
+    const int koct = __float_as_int(rec[4]), o = __float_as_int(rec[5]), layer = __float_as_int(rec[6]);
+    const int py = __float_as_int(rec[7]), px = __float_as_int(rec[8]);
+    const float* tab = sb.consts + EXPTAB_OFF;
+    const float scl_octv = ksize * 0.5f / (float)(1 << o);
+    const float* img = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
+    const int wd = sb.oct_w[o], ht = sb.oct_h[o];
+    const int radius = __float2int_rn(SIFT_ORI_RADIUS * scl_octv);
+    const float sigma = SIFT_ORI_SIG_FCTR * scl_octv;
+    const int n = SIFT_ORI_HIST_BINS;
+    const float expf_scale = -1.f / (2.f * sigma * sigma);
+    const int side = 2 * radius + 1, total = side * side;
+    float th = 0.f;                                   // temphist[lane] for lane < 36
+    for (int base = 0; base < total; base += 64) {
+        const int pos = base + lane;
+        bool valid = false;
+        int bin = 0;
+        float val = 0.f;
+        if (pos < total) {
+            const int ii = pos / side;
+            const int i = ii - radius, j = pos - ii * side - radius;
+            const int y = py + i, x = px + j;
+            valid = y > 0 && y < ht - 1 && x > 0 && x < wd - 1;
+            if (valid) {
+                const float dx = DAT(img, wd, y, x + 1) - DAT(img, wd, y, x - 1);
+                const float dy = DAT(img, wd, y - 1, x) - DAT(img, wd, y + 1, x);
+                const float wt = exp32f((float)(i * i + j * j) * expf_scale, tab);
+                const float ori = fast_atan2(dy, dx);
+                const float mag = sqrtf(dx * dx + dy * dy);
+                bin = __float2int_rn((n / 360.f) * ori);
+                if (bin >= n) bin -= n;
+                if (bin < 0) bin += n;
+                val = wt * mag;
+            }
+        }
+        const uint64_t m = __ballot(valid);
+        const int nv = __popcll(m);
+        if (valid) {
+            const int slot = __popcll(m & ((1ull << lane) - 1ull));
+            pbin[slot] = bin;
+            pval[slot] = val;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // four pixels per step (entries past nv are masked to 0, which leaves th unchanged)
+        for (int p0 = 0; p0 < nv; p0 += 4) {
+            const int4 bb = *reinterpret_cast<const int4*>(pbin + p0);
+            const float4 vv = *reinterpret_cast<const float4*>(pval + p0);
+            th += (p0 + 0 < nv && bb.x == lane) ? vv.x : 0.f;
+            th += (p0 + 1 < nv && bb.y == lane) ? vv.y : 0.f;
+            th += (p0 + 2 < nv && bb.z == lane) ? vv.z : 0.f;
+            th += (p0 + 3 < nv && bb.w == lane) ? vv.w : 0.f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    float* t2 = th_s[w];                              // temphist[-2 .. n+1] at t2[0 .. n+3]
+    if (lane < n) t2[2 + lane] = th;
+    if (lane == n - 1) t2[1] = th;                    // temphist[-1] = temphist[n-1]
+    if (lane == n - 2) t2[0] = th;                    // temphist[-2] = temphist[n-2]
+    if (lane == 0) t2[n + 2] = th;                    // temphist[n] = temphist[0]
+    if (lane == 1) t2[n + 3] = th;                    // temphist[n+1] = temphist[1]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float hv = -FLT_MAX;
+    if (lane < n) {
+        const float* t = t2 + 2 + lane;
+        hv = (t[-2] + t[2]) * (1.f / 16.f) + (t[-1] + t[1]) * (4.f / 16.f) + t[0] * (6.f / 16.f);
+        hs_s[w][lane] = hv;
+    }
+    float omax = hv;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off, 64));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
+    if (lane < n) {
+        const float* hist = hs_s[w];
+        const int j = lane;
+        const int l = j > 0 ? j - 1 : n - 1;
+        const int r2 = j < n - 1 ? j + 1 : 0;
+        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+            float angle = 360.f - (float)((360.f / n) * bin);
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            const int qo = atomicAdd(&sb.counters[1], 1);
+            if (qo < sb.kp_cap) {
+                float* out = sb.kp + 8 * (int64_t)qo;
+                out[0] = kx; out[1] = ky; out[2] = ksize; out[3] = angle; out[4] = kresp;
+                out[5] = __int_as_float(koct); out[6] = 0.f; out[7] = 0.f;
+            } else {
+                sb.counters[3] = 1;
+            }
+        }
+    }
+}
+
 // KeyPoint12_LessThan: x asc, y asc, size desc, angle asc, response desc, octave desc
 VO_DEV bool kp_less(const float* a, const float* b)
 {
@@ -528,7 +672,8 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
                       (1ull << 60) | (1ull << 61))
 __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
 {
-    __shared__ int pidx_s[4][64];
+    __shared__ int4 pidx_s4[4][16];
+    int (*pidx_s)[64] = reinterpret_cast<int (*)[64]>(pidx_s4);
     __shared__ float pval_s[4][64 * 8];
     __shared__ float hist_s[4][384];
     __shared__ float dst_s[4][128];
@@ -618,21 +763,35 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int p = 0; p < nv; ++p) {
-            const int id = pidx[p];
-            const int off = (lane - id) & 63;
-            const bool hit = (SIFT_HITMASK >> off) & 1ull;
-            // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
-            const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
-            const float v = hit ? pval[p * 8 + sl] : 0.f;
-            const int real = off + (off == 6 || off == 7 ? 64 : 0);
-            const int k = (id + real - lane) >> 6;
-            h0 += k == 0 ? v : 0.f;
-            h1 += k == 1 ? v : 0.f;
-            h2 += k == 2 ? v : 0.f;
-            h3 += k == 3 ? v : 0.f;
-            h4 += k == 4 ? v : 0.f;
-            h5 += k == 5 ? v : 0.f;
+        // four pixels per step: their LDS reads are issued together, the additions stay in
+        // pixel order (pidx is padded to a multiple of 4 with a bin no lane owns... see below)
+        for (int p0 = 0; p0 < nv; p0 += 4) {
+            const int4 ids = *reinterpret_cast<const int4*>(pidx + p0);
+            const int idv[4] = {ids.x, ids.y, ids.z, ids.w};
+            float vv4[4];
+            int kk4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int id = idv[u];
+                const int off = (lane - id) & 63;
+                const bool hit = p0 + u < nv && ((SIFT_HITMASK >> off) & 1ull);
+                // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
+                const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
+                vv4[u] = hit ? pval[(p0 + u) * 8 + sl] : 0.f;
+                const int real = off + (off == 6 || off == 7 ? 64 : 0);
+                kk4[u] = (id + real - lane) >> 6;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float v = vv4[u];
+                const int k = kk4[u];
+                h0 += k == 0 ? v : 0.f;
+                h1 += k == 1 ? v : 0.f;
+                h2 += k == 2 ? v : 0.f;
+                h3 += k == 3 ? v : 0.f;
+                h4 += k == 4 ? v : 0.f;
+                h5 += k == 5 ? v : 0.f;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -888,7 +1047,7 @@ extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, 
     const int* ks = SC.ks;
     if (hipMemcpyAsync(sb->consts, SC.host, sizeof(float) * (EXPTAB_OFF + 64), hipMemcpyHostToDevice, st) != hipSuccess)
         return VO_EHIP;
-    if (hipMemsetAsync(sb->counters, 0, 4 * sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
+    if (hipMemsetAsync(sb->counters, 0, 8 * sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
     // base: 2x upsample + blur to sigma
     float* g0 = sb->gauss + sb->gauss_off[0];
     hipLaunchKernelGGL(k_upsample, dim3((2 * W + 127) / 128, 2 * H), dim3(128), 0, st, img, W, H, g0);
@@ -922,7 +1081,13 @@ extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, 
             hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER), dim3(128), 0,
                                st, *sb, o, i);
     }
-    hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
+    const char* kser = getenv("VO_SIFT_KP_SERIAL");
+    if (kser && atoi(kser) == 1) {
+        hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
+    } else {
+        hipLaunchKernelGGL(k_sift_refine, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_ori, dim3((sb->cand_cap + 3) / 4), dim3(256), 0, st, *sb);
+    }
     hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1), dim3(1024), 0, st, *sb);
     // wave-per-keypoint descriptor kernel unless VO_SIFT_DESC_SERIAL=1 (thread per keypoint;
     // both produce identical descriptors)

@@ -26,7 +26,7 @@ class Sift:
             "dog": torch.empty(sb.dog_floats, dtype=torch.float32, device=dev),
             "tmp": torch.empty(sb.tmp_floats, dtype=torch.float32, device=dev),
             "consts": torch.zeros(7 * 32 + 64, dtype=torch.float32, device=dev),
-            "counters": torch.zeros(4, dtype=torch.int32, device=dev),
+            "counters": torch.zeros(8, dtype=torch.int32, device=dev),
             "cand": torch.empty(cand_cap * 4, dtype=torch.int32, device=dev),
             "kp": torch.empty(kp_cap * 8, dtype=torch.float32, device=dev),
             "kp_out": torch.zeros(kp_cap, 6, dtype=torch.float32, device=dev),

@@ -99,14 +99,18 @@ def test_sift_desc_wave_equals_serial(monkeypatch):
         img = torch.from_numpy(np.ascontiguousarray(fr[0])).cuda()
         sift = Sift(img.shape[1], img.shape[0], "cuda")
         out = {}
-        for mode in ("1", "0"):
-            monkeypatch.setenv("VO_SIFT_DESC_SERIAL", mode)
+        # (orientation stage, descriptor stage): serial thread-per-item kernels vs wave kernels
+        for kp_mode, desc_mode in (("1", "1"), ("1", "0"), ("0", "1"), ("0", "0")):
+            monkeypatch.setenv("VO_SIFT_KP_SERIAL", kp_mode)
+            monkeypatch.setenv("VO_SIFT_DESC_SERIAL", desc_mode)
             sift.run(img)
             kp, desc = sift.result()
-            out[mode] = (kp.copy(), desc.copy())
-        assert len(out["0"][0]) > 500
-        assert np.array_equal(out["0"][0], out["1"][0])
-        assert np.array_equal(out["0"][1], out["1"][1]), f"{preset}: descriptors differ"
+            out[kp_mode + desc_mode] = (kp.copy(), desc.copy())
+        ref = out["11"]
+        assert len(ref[0]) > 500
+        for key, (kp, desc) in out.items():
+            assert np.array_equal(kp, ref[0]), f"{preset} {key}: keypoints differ"
+            assert np.array_equal(desc, ref[1]), f"{preset} {key}: descriptors differ"
 
 
 def test_essential_and_recover_pose():
