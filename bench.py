@@ -148,6 +148,40 @@ def matcher_leg(device, pairs, n, iters=10):
             "flop_per_launch": 2.0 * n * n * 128 * pairs}
 
 
+def c3_leg(device, n_pairs=16, iters=2):
+    """BASELINE config C3 ("Malaga 1024x768, stresses SIFT + BF-match MFMA path"): n_pairs + 1
+    consecutive synthetic 1024x768 frames; SIFT detectAndCompute on every frame (vo_sift), then
+    one batched 2-NN over all consecutive pairs (vo_bf_knn2_batch), timed with HIP events.
+    pairs/s = one new frame's SIFT + one match per pair."""
+    from monocular_visual_odometry_va4mr_amd.features import Sift, bf_knn2_batch
+    rend = Renderer("malaga1024", seed=2, device=device)
+    Rs, cs = poses(n_pairs + 1, rend.p)
+    frames = rend.render_batch(list(range(n_pairs + 1)), Rs, cs)
+    sift = Sift(rend.W, rend.H, device)
+    D = torch.zeros((n_pairs + 1, sift.kp_cap, 128), dtype=torch.float32, device=device)
+    N = torch.zeros(n_pairs + 1, dtype=torch.int32, device=device)
+
+    def run():
+        for i in range(n_pairs + 1):
+            _, desc, n = sift.run(frames[i])
+            D[i].copy_(desc)
+            N[i:i + 1].copy_(n)
+        return bf_knn2_batch(D[:-1], N[:-1], D[1:], N[1:])
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return {"config": f"C3 malaga1024 synthetic, {n_pairs} consecutive pairs: SIFT per frame + batched BF 2-NN",
+            "pairs_per_s": round(n_pairs / (ms * 1e-3), 1), "ms_per_pair": round(ms / n_pairs, 3),
+            "keypoints_mean": round(float(N.float().mean()), 1)}
+
+
 def cpu_baseline(K, opts, frames_np, gap):
     """CPU restatement (oracle/, 1 thread) on one chain: bootstrap (untimed) then the
     per-frame step; median frame time after 10 warm-up frames."""
@@ -391,6 +425,7 @@ def main():
         out["cpu_baseline"] = None
     if world == 1 and not args.no_match:
         out["roofline_matcher"] = matcher_leg(device, args.match_pairs, args.match_n)
+        out["c3_sift_match"] = c3_leg(device)
     print(json.dumps(out))
     if args.stages:
         print(json.dumps({"stages_ms": stage, "bytes": bytes_by}), file=sys.stderr)

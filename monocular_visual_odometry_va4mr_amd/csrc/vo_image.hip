@@ -35,6 +35,9 @@ namespace {
 // zero-initialised and only interior pixels are stored (zeros fill partial vectors).
 #define PT_W 128
 #define PT_H 16
+#ifndef PYR0_TH
+#define PYR0_TH 32                          // level-0 tile rows
+#endif
 #define PV_W (PT_W + 8)                     // tile cols px0-4 .. px0+PT_W+3
 #define PV_H (PT_H + 2)                     // tile rows py0-1 .. py0+PT_H
 #define PS_H (2 * PV_H + 3)                 // staged source rows (level >= 1)
@@ -56,21 +59,22 @@ struct PyrLevelArgs {
 
 // L0: level 0 (frame bytes; its instantiation carries no source-staging LDS, so more blocks
 // fit per CU)
-template <bool L0>
+template <bool L0, int TH>
 __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
 {
-    __shared__ uint32_t PVw[PV_H * PV_W / 4];
-    __shared__ int yk[PV_H], xc[PV_W];
+    constexpr int PH = TH + 2, SH = 2 * PH + 3, RPT = TH / 8;   // tile rows + halo, staged source rows, rows / thread
+    __shared__ uint32_t PVw[PH * PV_W / 4];
+    __shared__ int yk[PH], xc[PV_W];
     __shared__ int mm[4];
     uint8_t* PV = (uint8_t*)PVw;
     const int tid = threadIdx.x;
     const int b = blockIdx.z;
-    const int px0 = blockIdx.x * PT_W, py0 = blockIdx.y * PT_H;
+    const int px0 = blockIdx.x * PT_W, py0 = blockIdx.y * TH;
     const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
     // level coordinates of the tile's rows / cols (-1: outside the padded level)
     if (tid < 4) mm[tid] = (tid & 1) ? -1 : 0x7fffffff;
     __syncthreads();
-    if (tid < PV_H) {
+    if (tid < PH) {
         const int py = py0 - 1 + tid;
         const int y = (py >= 0 && py < ph) ? refl101(py - VO_BORDER, A.h) : -1;
         yk[tid] = y;
@@ -85,7 +89,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
     __syncthreads();
     // every load of a phase is issued before the first one is consumed (fixed trip counts,
     // unrolled): the staging is latency-bound otherwise
-    constexpr int NPV = (PV_H * PV_W + 255) / 256;
+    constexpr int NPV = (PH * PV_W + 255) / 256;
     if constexpr (L0) {
         const uint8_t* fr = A.src + (int64_t)b * A.sstride;
         uint32_t v[NPV];
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         for (int i = 0; i < NPV; ++i) {
             const int e = tid + 256 * i;
             // unconditional load from a clamped address (keeps the loads in one batch)
-            const int ee = min(e, PV_H * PV_W - 1);
+            const int ee = min(e, PH * PV_W - 1);
             const int k = ee / PV_W, c = ee - k * PV_W;
             const int y = yk[k], x = xc[c];
             v[i] = fr[(int64_t)max(y, 0) * A.w + max(x, 0)];
@@ -102,11 +106,11 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
 #pragma unroll
         for (int i = 0; i < NPV; ++i) {
             const int e = tid + 256 * i;
-            if (e < PV_H * PV_W) PV[e] = (uint8_t)v[i];
+            if (e < PH * PV_W) PV[e] = (uint8_t)v[i];
         }
     } else {
-        __shared__ uint32_t SRw[PS_H * PS_W / 4];
-        __shared__ uint16_t HS[PS_H * PV_W];
+        __shared__ uint32_t SRw[SH * PS_W / 4];
+        __shared__ uint16_t HS[SH * PV_W];
         const uint8_t* SR = (const uint8_t*)SRw;
         // source rectangle (level l-1 coordinates) under the tile
         const int sy0 = 2 * mm[0] - 2, sy1 = 2 * mm[1] + 2;
@@ -116,7 +120,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         const int ax0 = gx0 & ~3, sh = gx0 - ax0;
         const int nwd = (sx1 + VO_BORDER - ax0) / 4 + 1; // dwords per staged row
         const uint8_t* sbase = A.src + (int64_t)b * A.sstride + A.soff + ax0;
-        constexpr int NSR = (PS_H * (PS_W / 4) + 255) / 256;
+        constexpr int NSR = (SH * (PS_W / 4) + 255) / 256;
         uint32_t v[NSR];
 #pragma unroll
         for (int i = 0; i < NSR; ++i) {
@@ -128,7 +132,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
 #pragma unroll
         for (int i = 0; i < NSR; ++i) {
             const int e = tid + 256 * i;
-            if (e < PS_H * (PS_W / 4)) SRw[e] = v[i];
+            if (e < SH * (PS_W / 4)) SRw[e] = v[i];
         }
         __syncthreads();
         // horizontal [1 4 6 4 1] at the tile's columns, every staged row
@@ -143,7 +147,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
             HS[r * PV_W + c] = v;
         }
         __syncthreads();
-        for (int e = tid; e < PV_H * PV_W; e += 256) {
+        for (int e = tid; e < PH * PV_W; e += 256) {
             const int k = e / PV_W, c = e - k * PV_W;
             const int y = yk[k];
             uint8_t v = 0;
@@ -156,13 +160,13 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         }
     }
     __syncthreads();
-    // 4 pixels x 2 rows per thread: pyramid dword stores, then the Scharr of interior pixels
+    // 4 pixels x RPT rows per thread: pyramid dword stores, then the Scharr of interior pixels
     const int tc = tid & 31, tr = tid >> 5;
     const int px = px0 + 4 * tc;
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-        const int k = 1 + 2 * tr + rr;
-        const int py = py0 + 2 * tr + rr;
+    for (int rr = 0; rr < RPT; ++rr) {
+        const int k = 1 + RPT * tr + rr;
+        const int py = py0 + RPT * tr + rr;
         if (py >= ph || px >= A.pitch) continue;
         const uint32_t* rowc = PVw + (k * PV_W) / 4 + 1 + tc;      // cols px..px+3
         *(uint32_t*)(A.pyr + (int64_t)b * A.pstride + A.off + (int64_t)py * A.pitch + px) = rowc[0];
@@ -1983,9 +1987,14 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
         A.level = l;
         const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
         if (A.pitch % 64 || A.pitch < pw) return VO_EARG;
-        dim3 g((pw + PT_W - 1) / PT_W, (ph + PT_H - 1) / PT_H, d->B);
-        if (l == 0) hipLaunchKernelGGL(k_pyr_level<true>, g, dim3(256), 0, VO_STREAM(stream), A);
-        else hipLaunchKernelGGL(k_pyr_level<false>, g, dim3(256), 0, VO_STREAM(stream), A);
+        // level 0 (frame bytes, small LDS): 32-row tiles, half the blocks; pyrDown levels: 16
+        if (l == 0) {
+            dim3 g((pw + PT_W - 1) / PT_W, (ph + PYR0_TH - 1) / PYR0_TH, d->B);
+            hipLaunchKernelGGL((k_pyr_level<true, PYR0_TH>), g, dim3(256), 0, VO_STREAM(stream), A);
+        } else {
+            dim3 g((pw + PT_W - 1) / PT_W, (ph + PT_H - 1) / PT_H, d->B);
+            hipLaunchKernelGGL((k_pyr_level<false, PT_H>), g, dim3(256), 0, VO_STREAM(stream), A);
+        }
     }
     return hip_ok() ? VO_OK : VO_EHIP;
 }
