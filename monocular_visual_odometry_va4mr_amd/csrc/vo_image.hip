@@ -794,11 +794,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // one exact 32-bit reduction each unless a lane's partial could overflow the sum
                 const bool twide = __ballot((uint32_t)a11 >= (1u << 25) || (uint32_t)a22 >= (1u << 25) ||
                                             (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
-                int64_t iA11, iA12, iA22;
-                if (!twide) { iA11 = wave_sum_dpp(a11); iA12 = wave_sum_dpp(a12); iA22 = wave_sum_dpp(a22); }
-                else { iA11 = wave_sum_split(a11); iA12 = wave_sum_split(a12); iA22 = wave_sum_split(a22); }
                 const float FLT_SCALE = 1.f / (1 << 20);
-                const float A11 = (float)iA11 * FLT_SCALE, A12 = (float)iA12 * FLT_SCALE, A22 = (float)iA22 * FLT_SCALE;
+                float A11, A12, A22;
+                if (!twide) {
+                    A11 = (float)wave_sum_dpp(a11) * FLT_SCALE; A12 = (float)wave_sum_dpp(a12) * FLT_SCALE;
+                    A22 = (float)wave_sum_dpp(a22) * FLT_SCALE;
+                } else {
+                    A11 = (float)wave_sum_split(a11) * FLT_SCALE; A12 = (float)wave_sum_split(a12) * FLT_SCALE;
+                    A22 = (float)wave_sum_split(a22) * FLT_SCALE;
+                }
                 float D = A11 * A22 - A12 * A12;
                 const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
                 if (minEig < P.min_eig || D < FLT_EPSILON) {
@@ -822,9 +826,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     }
                     a = nx - inx;
                     bb = ny - iny;
-                    const int w00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
-                    const int w01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
-                    const int w10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
+                    // wave-uniform weights: into scalar registers, packed by the scalar unit
+                    const int w00 = __builtin_amdgcn_readfirstlane(__float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14)));
+                    const int w01 = __builtin_amdgcn_readfirstlane(__float2int_rn(a * (1.f - bb) * (float)(1 << 14)));
+                    const int w10 = __builtin_amdgcn_readfirstlane(__float2int_rn((1.f - a) * bb * (float)(1 << 14)));
                     const int w11 = (1 << 14) - w00 - w01 - w10;
                     // iw11 can be -1: dot with w11 + 1 and subtract the tap once
                     const int neg = w11 < 0;
@@ -844,11 +849,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     }
                     const bool wide = __ballot((uint32_t)(b1 + (1 << 24)) >= (1u << 25) ||
                                                (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
-                    int64_t s1, s2;
-                    if (!wide) { s1 = wave_sum_dpp(b1); s2 = wave_sum_dpp(b2); }
-                    else { s1 = wave_sum_split(b1); s2 = wave_sum_split(b2); }
-                    const float fb1 = (float)s1 * FLT_SCALE;
-                    const float fb2 = (float)s2 * FLT_SCALE;
+                    // int32 -> float and int64 -> float round the same integer identically
+                    float fb1, fb2;
+                    if (!wide) { fb1 = (float)wave_sum_dpp(b1) * FLT_SCALE; fb2 = (float)wave_sum_dpp(b2) * FLT_SCALE; }
+                    else { fb1 = (float)wave_sum_split(b1) * FLT_SCALE; fb2 = (float)wave_sum_split(b2) * FLT_SCALE; }
                     const float ddx = (A12 * fb2 - A22 * fb1) * D;
                     const float ddy = (A12 * fb1 - A11 * fb2) * D;
                     nx += ddx;
