@@ -818,7 +818,10 @@ __global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
     int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
     const float* cor = s.corners + (int64_t)b * d.mcap * 2;
     const float mdf = (float)A.min_dist;
-    const int cs = (int)ceil(A.min_dist) > 0 ? (int)ceil(A.min_dist) : 1;
+    // cells of at least minDistance: the 3x3 neighbourhood holds every candidate within it.
+    // Coarser cells keep that exact, so they grow until the grid fits the LDS tables.
+    int cs = (int)ceil(A.min_dist) > 0 ? (int)ceil(A.min_dist) : 1;
+    while ((d.W / cs + 3) * (d.H / cs + 3) > ADD_MAX_CELLS) ++cs;
     const int gw = d.W / cs + 3, gh = d.H / cs + 3;
     const bool grid = (gw * gh <= ADD_MAX_CELLS) && (P <= ADD_MAX_ITEMS);
     if (grid) {

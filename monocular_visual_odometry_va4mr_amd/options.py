@@ -37,9 +37,14 @@ _MALAGA = dict(_KITTI, min_dist_landmarks=0, max_dist_landmarks=100, feature_qua
 _PARKING = dict(_KITTI, max_dist_landmarks=50, maxLevel=10,
                 criteria=(TERM_CRITERIA_EPS | TERM_CRITERIA_COUNT, 50, 0.02), PnP_error=5)
 
+# BASELINE config C5: 1920x1080 roofline run, KITTI options otherwise, GFTT
+# tuned to yield ~8k corners per frame (maxCorners 8192, qualityLevel 0.01, minDistance 5)
+_HD1080_C5 = dict(_KITTI, feature_max_corners=8192, feature_quality_level=0.01, feature_min_dist=5)
+
 PRESETS = {
     # name: (options, bootstrap_frames, last_frame)
     'kitti': (_KITTI, (0, 2), 2761),
+    'hd1080': (_HD1080_C5, (0, 2), 10000),
     'malaga': (_MALAGA, (0, 6), 2120),
     'parking': (_PARKING, (0, 6), 598),
 }
@@ -50,7 +55,7 @@ SEQ_TO_OPTIONS = {
     'parking': 'parking',
     'malaga': 'malaga',
     'malaga1024': 'malaga',
-    'hd1080': 'kitti',
+    'hd1080': 'hd1080',
 }
 
 
