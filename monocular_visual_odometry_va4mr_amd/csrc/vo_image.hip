@@ -1562,6 +1562,7 @@ struct SelParams {
     int acc_lds;             // accepted-corner slots in LDS (min(mcap, ACC_MAX))
     int grid_lds;            // grid cells held in LDS (0: grid in L2)
     int64_t gstride;
+    int grid_glb;            // the parallel walk may keep its grid + cell lists in gscratch
     const int32_t* chain_status;
 };
 
@@ -1569,8 +1570,15 @@ struct SelParams {
 // geometric bound (cell = round(minDistance) <= minDistance + 0.5) allows at most two.
 VO_DEV uint32_t cell_get(bool lds, uint32_t* lg, uint32_t* gg, int c)
 {
-    return lds ? lg[c] : atomicOr(&gg[c], 0u);   // atomics are L2-coherent
+    // the L2 copy is only written by atomics: read it at agent scope (past the CU's L1)
+    return lds ? lg[c] : __hip_atomic_load(&gg[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+VO_DEV int head_get(bool lds, int* lh, int* gh, int c)
+{
+    return lds ? lh[c] : __hip_atomic_load(&gh[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the parallel walk's L2 grid + cell-list heads sit after the conflict lists in gscratch
+#define SEL_GG_OFF (PAGE * 8)
 VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
 {
     if (lds) lg[c] = v;
@@ -1633,9 +1641,14 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
     const int cap = P.mcap < P.acc_lds ? P.mcap : P.acc_lds;
     const int limit = want < cap ? want : cap;
     const bool lds = (int64_t)gw * gh <= P.grid_lds;
-    uint32_t* gg = P.gscratch + (int64_t)b * P.gstride;
+    // parallel walk: grid in LDS, or (P.grid_glb) grid + cell-list heads in gscratch
+    const bool par = use_grid && (lds || P.grid_glb);
+    uint32_t* gg = P.gscratch + (int64_t)b * P.gstride + (lds || !P.grid_glb ? 0 : SEL_GG_OFF);
+    int* ghead = (int*)(gg + gw * gh);
     if (use_grid) {
         for (int q = tid; q < gw * gh; q += blockDim.x) cell_set(lds, lgrid, gg, q, 0xFFFFFFFFu);
+        if (par && !lds)
+            for (int q = tid; q < gw * gh; q += blockDim.x) atomicExch(&ghead[q], -1);
     }
     float* out = P.corners + (int64_t)b * P.mcap * 2;
     int nacc = 0;
@@ -1703,7 +1716,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
         }
         SELPROF(3);
         const uint64_t page_last = page[take - 1];
-        if (use_grid && lds) {
+        if (par) {
             // ---- exact parallel form of OpenCV's sequential minDistance walk.  Candidate i
             // (rank order) is accepted iff no earlier accepted candidate in its 3x3 cell
             // neighbourhood is closer than minDistance, and no corner accepted on an earlier
@@ -1715,7 +1728,8 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                 const int y = (int)(addr / (uint32_t)P.W), x = (int)(addr - (uint32_t)y * P.W);
                 cand_xy[i] = (uint32_t)x | ((uint32_t)y << 16);
             }
-            for (int q = tid; q < gw * gh; q += blockDim.x) head[q] = -1;
+            if (lds)
+                for (int q = tid; q < gw * gh; q += blockDim.x) head[q] = -1;
             __syncthreads();
             int* nxt = (int*)page;                                // page keys are dead now
             volatile uint8_t* stt = (volatile uint8_t*)(nxt + PAGE);
@@ -1729,7 +1743,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                     const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
                     for (int yy = y1; yy <= y2; ++yy)
                         for (int xx = x1; xx <= x2; ++xx) {
-                            const uint32_t cv = lgrid[yy * gw + xx];
+                            const uint32_t cv = cell_get(lds, lgrid, gg, yy * gw + xx);
                             for (int q = 0; q < 2; ++q) {
                                 const uint32_t id = (cv >> (16 * q)) & 0xFFFFu;
                                 if (id == 0xFFFFu) break;
@@ -1741,7 +1755,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                         }
                 }
                 stt[i] = rej ? 2 : 0;                             // 0 undecided, 1 accepted, 2 rejected
-                nxt[i] = atomicExch(&head[yc * gw + xc], i);
+                nxt[i] = lds ? atomicExch(&head[yc * gw + xc], i) : atomicExch(&ghead[yc * gw + xc], i);
             }
             __syncthreads();
             // each candidate's earlier conflicts (same test as OpenCV's walk), found once:
@@ -1760,7 +1774,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                 int c = 0;
                 for (int yy = y1; yy <= y2; ++yy)
                     for (int xx = x1; xx <= x2; ++xx)
-                        for (int j = head[yy * gw + xx]; j >= 0; j = nxt[j]) {
+                        for (int j = head_get(lds, head, ghead, yy * gw + xx); j >= 0; j = nxt[j]) {
                             if (j >= i) continue;
                             const uint32_t aa = cand_xy[j];
                             const float ddx = (float)x - (float)(aa & 0xFFFF);
@@ -1796,7 +1810,7 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                         const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
                         for (int yy = y1; yy <= y2 && !rej; ++yy)
                             for (int xx = x1; xx <= x2 && !rej; ++xx)
-                                for (int j = head[yy * gw + xx]; j >= 0; j = nxt[j]) {
+                                for (int j = head_get(lds, head, ghead, yy * gw + xx); j >= 0; j = nxt[j]) {
                                     if (j >= i) continue;
                                     const uint8_t sj = stt[j];
                                     if (sj == 2) continue;
@@ -1836,16 +1850,23 @@ __global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
                     out[2 * pos + 1] = (float)y;
                     // at most two corners share a cell; slot order inside a cell is irrelevant
                     const int cell = (y / cs) * gw + (x / cs);
-                    uint32_t cur = lgrid[cell];
+                    uint32_t cur = cell_get(lds, lgrid, gg, cell);
                     for (;;) {
                         const uint32_t nv = ((cur & 0xFFFFu) == 0xFFFFu) ? ((cur & 0xFFFF0000u) | (uint32_t)pos)
                                                                         : ((cur & 0xFFFFu) | ((uint32_t)pos << 16));
-                        const uint32_t prev = atomicCAS(&lgrid[cell], cur, nv);
+                        const uint32_t prev = lds ? atomicCAS(&lgrid[cell], cur, nv) : atomicCAS(&gg[cell], cur, nv);
                         if (prev == cur) break;
                         cur = prev;
                     }
                 }
                 nacc = min(nacc + tot, limit);
+            }
+            if (!lds) {
+                // empty the cell lists this page used (the next page rebuilds them)
+                for (int i = tid; i < take; i += blockDim.x) {
+                    const uint32_t xy = cand_xy[i];
+                    atomicExch(&ghead[((int)(xy >> 16) / cs) * gw + (int)(xy & 0xFFFF) / cs], -1);
+                }
             }
             if (tid == 0) sh_int[2] = nacc;
         } else {
@@ -2187,8 +2208,11 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
         const int64_t cells = md >= 1 ? (int64_t)((d->W + cs - 1) / cs) * ((d->H + cs - 1) / cs) : 0;
         S.acc_lds = d->mcap < ACC_MAX ? d->mcap : ACC_MAX;
         S.grid_lds = cells <= GRID_LDS_CELLS ? (int)cells : 0;
-        // grid + per-cell candidate lists in LDS when they fit, else the L2 grid path
+        // grid + per-cell candidate lists in LDS when they fit, else in the eigen-map scratch
+        // (after the conflict lists) for the same parallel walk, else the wave-serial L2 path
         if (12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds > 150 * 1024) S.grid_lds = 0;
+        static const int noglb = [] { const char* e = getenv("VO_SEL_SERIAL_L2"); return e ? atoi(e) : 0; }();
+        S.grid_glb = !noglb && S.grid_lds == 0 && SEL_GG_OFF + 2 * cells <= S.gstride;
         const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
         static const bool attr_ok = hipFuncSetAttribute((const void*)k_gftt_select,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize,

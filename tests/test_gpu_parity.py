@@ -108,7 +108,10 @@ def O_refl(p, n):
 def test_gftt_bitexact(kitti_frames, engine_factory):
     from oracle import _olib as O
     fr, K = kitti_frames
-    for q, md, mc in [(0.1, 10, 1400), (0.01, 10, 1400), (0.05, 5.0, 300)]:
+    # md 2 / 1.6: minDistance grid too large for LDS -> the parallel walk on the L2 grid;
+    # md 1: the grid does not fit the scratch either -> the wave-serial L2 walk
+    for q, md, mc in [(0.1, 10, 1400), (0.01, 10, 1400), (0.05, 5.0, 300), (0.01, 2.0, 6000),
+                      (0.001, 1.6, 8000), (0.01, 1.0, 3000)]:
         eng, opts = engine_factory(K=K, feature_quality_level=q, feature_min_dist=md, feature_max_corners=mc)
         eng.build_pyramid(fr[1], 0)
         L = eng.lib
