@@ -22,6 +22,8 @@ Extra JSON fields:
                   algorithmic bytes (DESIGN.md "Kernels") / mean stage time
   cpu_baseline -- the CPU restatement (oracle/, OpenCV-4.6 semantics, 1 core) timed per
                   frame on this host over a bounded sample (rank 0, N=1 only)
+  cpu_baseline_threads -- the same restatement on up to 16 chains at once, one host thread
+                  each: the multi-core CPU rate (aggregate frames/s)
   ate_vs_ref   -- ATE of the GPU trajectory vs that CPU run on the same frames
 """
 from __future__ import annotations
@@ -62,6 +64,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="chains in the multi-thread CPU leg (1: skip)")
+    ap.add_argument("--cpu-mt-frames", type=int, default=30, help="steps per chain in the multi-thread CPU leg")
     ap.add_argument("--no-single", action="store_true", help="skip the single-chain latency / CPU leg "
                     "(profiling runs of the batched workload)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -244,6 +248,33 @@ def cpu_baseline(K, opts, frames_np, gap):
     med = float(np.median(ts[10:] if len(ts) > 20 else ts))
     pos = np.array([np.asarray(t, np.float64).ravel() for _, t in s.transforms])
     return med, wall, len(ts), pos
+
+
+def cpu_baseline_threads(K, opts, frames_np, threads):
+    """The same CPU restatement on `threads` independent chains at once (one Python thread per
+    chain; the oracle's C stages release the GIL), bootstraps untimed: aggregate frames/s."""
+    import threading
+    from oracle import vo_pipeline_oracle as V
+    bar = threading.Barrier(threads + 1)
+    res = [0] * threads
+
+    def run(i):
+        s = V.new_state(K, opts)
+        V.initialize(s, frames_np[0], frames_np[1])
+        bar.wait()
+        for f in range(2, len(frames_np)):
+            V.step(s, frames_np[f])
+        res[i] = len(frames_np) - 2
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for t in th:
+        t.start()
+    bar.wait()
+    t0 = time.perf_counter()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    return sum(res) / wall, wall
 
 
 def gpu_chain_positions(K, opts, frames_dev, device):
@@ -461,6 +492,18 @@ def main():
             out["cpu_baseline"] = {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": 1, "kind": "port",
                                    "sample": f"1 chain, {args.preset} frames 0,{gap} bootstrap + {n} steps; "
                                              f"median step after 10 warm-up ({wall:.1f}s total)"}
+            try:
+                ncpu = len(os.sched_getaffinity(0))
+            except AttributeError:
+                ncpu = os.cpu_count() or 1
+            thr = max(1, min(args.cpu_threads, ncpu))
+            if thr > 1:
+                nmt = min(len(fr_np), 2 + args.cpu_mt_frames)
+                fps_mt, wall_mt = cpu_baseline_threads(Kmat, opts, fr_np[:nmt], thr)
+                out["cpu_baseline_threads"] = {
+                    "value": round(fps_mt, 3), "unit": "frames/s", "cores": thr, "kind": "port",
+                    "sample": f"{thr} chains at once (one thread each), {nmt - 2} steps per chain after an "
+                              f"untimed bootstrap ({wall_mt:.1f}s)"}
             from monocular_visual_odometry_va4mr_amd.ate import ate
             rmse, rel = ate(pos_gpu, pos_cpu)
             out["ate_vs_ref"] = {"rmse": float(rmse), "rel_path": float(rel), "frames": int(len(pos_cpu)),
