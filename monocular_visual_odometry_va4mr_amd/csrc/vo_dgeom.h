@@ -175,67 +175,85 @@ VO_DEV void svd_jacobi_wave(double* A, double* w, double* V)
 }
 
 // Round-robin Jacobi SVD (oracle/vo_oracle_geom.c svd_jacobi_rr) by one wave, A [M*N], w [N],
-// V [N*N] and cs [N/2 * 3] in LDS, N even.  Round r pairs the columns by the circle method; the
-// N/2 pairs of a round are disjoint, so lane p < N/2 forms pair p's sums (scalar order) and
-// rotation, and then every lane applies all of the round's rotations to its row.
+// V [N*N] in LDS, N even.  Round r pairs the columns by the circle method; the N/2 pairs of a
+// round are disjoint.  Lane c < N keeps column c of A and of V in registers for all sweeps: per
+// round it fetches its partner's column with lane permutes, and both lanes of a pair form the
+// pair's sums in the scalar order, the same rotation, and each its own rotated column -- the
+// oracle's operations on the same values, so bit-identical, with no LDS traffic or wave
+// barrier inside the sweeps.  (cs is unused; kept for the callers' LDS layout.)
 template <int M, int N>
 VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
 {
     static_assert(N % 2 == 0 && N <= 64 && M <= 64, "round-robin SVD needs even N <= 64");
+    (void)cs;
     constexpr int NP = N / 2;
     const int lane = lane_id();
-    for (int q = lane; q < N * N; q += 64) V[q] = (q / N == q % N) ? 1.0 : 0.0;
-    wave_lds_sync();
+    const int col = lane < N ? lane : 0;
+    // partner of this lane's column in every round
+    int prt[N - 1];
+#pragma unroll
+    for (int r = 0; r < N - 1; ++r) {
+        prt[r] = col;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
+            const int b = ((N - 2 - q + r) % (N - 1)) + 1;
+            if (a == col) prt[r] = b;
+            if (b == col) prt[r] = a;
+        }
+    }
+    double x[M], v[N];
+#pragma unroll
+    for (int k = 0; k < M; ++k) x[k] = A[k * N + col];
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = k == col ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
         bool changed = false;
+#pragma unroll
         for (int r = 0; r < N - 1; ++r) {
-            if (lane < NP) {
-                const int q = lane;
-                const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
-                const int b = ((N - 2 - q + r) % (N - 1)) + 1;
-                const int i = a < b ? a : b, j = a < b ? b : a;
-                double alpha = 0, beta = 0, gamma = 0;
+            const int p = prt[r];
+            const bool lo = col < p;           // this lane holds column i (= min of the pair)
+            double px[M], pv[N];
+#pragma unroll
+            for (int k = 0; k < M; ++k) px[k] = __shfl(x[k], p, 64);
+#pragma unroll
+            for (int k = 0; k < N; ++k) pv[k] = __shfl(v[k], p, 64);
+            double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+                const double ai = lo ? x[k] : px[k], aj = lo ? px[k] : x[k];
+                alpha += ai * ai;
+                beta += aj * aj;
+                gamma += ai * aj;
+            }
+            if (alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta))) {
+                changed = true;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                if (zeta < 0) t = -t;
+                const double c = 1.0 / sqrt(1.0 + t * t);
+                const double s = c * t;
 #pragma unroll
                 for (int k = 0; k < M; ++k) {
-                    double ai = A[k * N + i], aj = A[k * N + j];
-                    alpha += ai * ai;
-                    beta += aj * aj;
-                    gamma += ai * aj;
+                    const double xi = lo ? x[k] : px[k], xj = lo ? px[k] : x[k];
+                    x[k] = lo ? c * xi - s * xj : s * xi + c * xj;
                 }
-                double c = 1.0, s = 0.0, f = 0.0;
-                if (alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta))) {
-                    double zeta = (beta - alpha) / (2.0 * gamma);
-                    double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                    if (zeta < 0) t = -t;
-                    c = 1.0 / sqrt(1.0 + t * t);
-                    s = c * t;
-                    f = 1.0;
-                }
-                cs[3 * q] = c;
-                cs[3 * q + 1] = s;
-                cs[3 * q + 2] = f;
-            }
-            wave_lds_sync();
-            // the NP rotations touch disjoint column pairs: apply them all at once, one
-            // (pair, row of A or V) item per lane
 #pragma unroll
-            for (int q = 0; q < NP; ++q) changed |= cs[3 * q + 2] != 0.0;
-            for (int it = lane; it < NP * (M + N); it += 64) {
-                const int q = it / (M + N), row = it - q * (M + N);
-                if (cs[3 * q + 2] == 0.0) continue;
-                const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
-                const int b = ((N - 2 - q + r) % (N - 1)) + 1;
-                const int i = a < b ? a : b, j = a < b ? b : a;
-                const double c = cs[3 * q], s = cs[3 * q + 1];
-                double* X = row < M ? A + row * N : V + (row - M) * N;
-                const double xi = X[i], xj = X[j];
-                X[i] = c * xi - s * xj;
-                X[j] = s * xi + c * xj;
+                for (int k = 0; k < N; ++k) {
+                    const double vi = lo ? v[k] : pv[k], vj = lo ? pv[k] : v[k];
+                    v[k] = lo ? c * vi - s * vj : s * vi + c * vj;
+                }
             }
-            wave_lds_sync();
         }
-        if (!changed) break;
+        if (__ballot(lane < N && changed) == 0) break;
     }
+    if (lane < N) {
+#pragma unroll
+        for (int k = 0; k < M; ++k) A[k * N + col] = x[k];
+#pragma unroll
+        for (int k = 0; k < N; ++k) V[k * N + col] = v[k];
+    }
+    wave_lds_sync();
     for (int i = 0; i < N; ++i) {
         double s = 0;
 #pragma unroll
