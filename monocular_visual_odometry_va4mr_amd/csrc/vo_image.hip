@@ -316,6 +316,13 @@ VO_DEV void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a wave-uniform VALU result into an SGPR: the readfirstlane of an opaque VALU value cannot
+// be moved ahead of the conversion that produced it, so the arithmetic that consumes it (the
+// weight packing) runs on the scalar unit instead of the VALU
+VO_DEV int to_sgpr(int v)
+{
+    return __builtin_amdgcn_readfirstlane(v + opaque0());
+}
 VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 {
     return (uint32_t)((w00 >> shift) & mask) | ((uint32_t)((w01 >> shift) & mask) << 8) |
@@ -827,9 +834,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     a = nx - inx;
                     bb = ny - iny;
                     // wave-uniform weights: into scalar registers, packed by the scalar unit
-                    const int w00 = __builtin_amdgcn_readfirstlane(__float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14)));
-                    const int w01 = __builtin_amdgcn_readfirstlane(__float2int_rn(a * (1.f - bb) * (float)(1 << 14)));
-                    const int w10 = __builtin_amdgcn_readfirstlane(__float2int_rn((1.f - a) * bb * (float)(1 << 14)));
+                    const int w00 = to_sgpr(__float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14)));
+                    const int w01 = to_sgpr(__float2int_rn(a * (1.f - bb) * (float)(1 << 14)));
+                    const int w10 = to_sgpr(__float2int_rn((1.f - a) * bb * (float)(1 << 14)));
                     const int w11 = (1 << 14) - w00 - w01 - w10;
                     // iw11 can be -1: dot with w11 + 1 and subtract the tap once
                     const int neg = w11 < 0;
