@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include <float.h>
+#include <type_traits>
 
 namespace {
 
@@ -586,11 +587,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     constexpr int IRS = QS / 4, JRS = 8;
     static_assert(JRW >= QM + 1 && JRW <= JRS && IRW <= IRS && IRW <= 8 && DRW == 16 && QS % 4 == 0,
                   "k_lk_w staging layout");
-    __shared__ uint4 QT4[TH * QM];
+    // one spare row in QT / IR / DR: read (never used) by the dead lanes of window row 15
+    __shared__ uint4 QT4[(TH + 1) * QM];
     const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
     __shared__ uint32_t JR[(TH + 1) * JRS];
-    __shared__ uint32_t IR[(WH + 1) * IRS];
-    __shared__ uint32_t DR[(WH + 1) * QS];
+    __shared__ uint32_t IR[(WH + 2) * IRS];
+    __shared__ uint32_t DR[(WH + 2) * QS];
     const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb, pcur = -1;
     const int lane = lane_id();
@@ -606,15 +608,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     if (n1 <= P.seg1_min) n1 = 0;
     const int ntot = n0 + n1;
     const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
-    // window pixel k = lane + 64 j; its offset in the QT tile is kept (the iterations read it),
-    // its row / column are recomputed where needed
+    // window pixels of a lane: column lane % 16, rows 4 j + s with s = (lane / 32) + 2 (lane / 16
+    // % 2), so that a 32-lane half reads rows s and s + 2 (row offsets 0 and 2 * QS = 48 dwords,
+    // 16 banks apart: conflict-free) and pixel j sits at the constant offset toff + 4 j QS
+    // (folded into the LDS instruction).  Column 15 and row 15 are dead lanes.
+    static_assert(WW <= 16 && WH <= 16 && MAXJ == 4 && (2 * QS) % 32 == 16, "k_lk_w window map");
+    const int wrow = ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1), wcol = lane & 15;
+    const int toff0 = wrow * QS + wcol;
     int toff[MAXJ];
     bool live[MAXJ];
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
-        const int k = lane + 64 * j;
-        live[j] = k < NPX;
-        toff[j] = live[j] ? (k / WW) * QS + k % WW : 0;
+        live[j] = wcol < WW && wrow + 4 * j < WH;
+        toff[j] = toff0 + 4 * j * QS;
     }
     int tx0 = 0, ty0 = 0, jsh = 0;
     int cols = 0, rows = 0, pitch = 0, loff = 0;
@@ -844,16 +850,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
                     const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int b1 = 0, b2 = 0;
+                    // the iw11 = -1 correction only in its own (wave-uniform) copy of the loop
+                    auto mismatch = [&](auto negc) {
 #pragma unroll
-                    for (int j = 0; j < MAXJ; ++j) {
-                        const uint32_t q = tb[toff[j]];
-                        uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
-                                       __builtin_amdgcn_udot4(q, wlo, 256u, false);
-                        if (neg) sum -= q >> 24;
-                        const int diff = (int)(sum >> 9) - ival[j];
-                        b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
-                        b2 += __mul24(diff, iyv[j]);
-                    }
+                        for (int j = 0; j < MAXJ; ++j) {
+                            const uint32_t q = tb[toff[j]];
+                            uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                                           __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                            if (decltype(negc)::value) sum -= q >> 24;
+                            const int diff = (int)(sum >> 9) - ival[j];
+                            b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
+                            b2 += __mul24(diff, iyv[j]);
+                        }
+                    };
+                    if (neg) mismatch(std::true_type());
+                    else mismatch(std::false_type());
                     const bool wide = __ballot((uint32_t)(b1 + (1 << 24)) >= (1u << 25) ||
                                                (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
                     // int32 -> float and int64 -> float round the same integer identically
