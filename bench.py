@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--prio", default="none", choices=["none", "g0", "side"], help="HIP stream priorities of the groups")
     ap.add_argument("--cpu-threads", type=int, default=16, help="chains in the multi-thread CPU leg (1: skip)")
     ap.add_argument("--cpu-mt-frames", type=int, default=30, help="steps per chain in the multi-thread CPU leg")
     ap.add_argument("--no-single", action="store_true", help="skip the single-chain latency / CPU leg "
@@ -355,7 +356,11 @@ def main():
     for g in range(G):
         engines.append(Engine(Kmat, opts, Wd, H, batch=bounds[g + 1] - bounds[g], device=device,
                               ncap=16384, pcap=16384, fcap=n_after + 16))
-        streams.append(torch.cuda.Stream(device) if G > 1 else torch.cuda.current_stream(device))
+        # --prio g0: group 0's streams at high priority, so its latency-bound stages are never
+        # queued behind another group's bulk launches (the other groups fill the idle CUs)
+        hi = args.prio == "g0" and g == 0 and G > 1
+        engines[-1].side_priority = -1 if (hi or args.prio == "side") else 0
+        streams.append(torch.cuda.Stream(device, priority=-1 if hi else 0) if G > 1 else torch.cuda.current_stream(device))
     eng = engines[0]
     torch.cuda.synchronize()
     t0 = time.perf_counter()

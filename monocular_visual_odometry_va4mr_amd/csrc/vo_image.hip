@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         }
     } else {
         __shared__ uint32_t SRw[SH * PS_W / 4];
-        __shared__ uint16_t HS[SH * PV_W];
+        __shared__ uint2 HSw[SH * PV_W / 4];                 // horizontal sums: u16 column quads
         const uint8_t* SR = (const uint8_t*)SRw;
         // source rectangle (level l-1 coordinates) under the tile
         const int sy0 = 2 * mm[0] - 2, sy1 = 2 * mm[1] + 2;
@@ -136,31 +136,64 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
             if (e < SH * (PS_W / 4)) SRw[e] = v[i];
         }
         __syncthreads();
-        // horizontal [1 4 6 4 1] at the tile's columns, every staged row
-        for (int e = tid; e < nsr * PV_W; e += 256) {
-            const int r = e / PV_W, c = e - r * PV_W;
-            const int x = xc[c];
-            uint16_t v = 0;
-            if (x >= 0) {
-                const uint8_t* q = SR + r * PS_W + sh + (2 * x - 2 - sx0);
-                v = (uint16_t)(q[0] + 4 * q[1] + 6 * q[2] + 4 * q[3] + q[4]);
+        // horizontal [1 4 6 4 1] at the tile's columns, every staged row: four columns per
+        // item.  Interior quads (four consecutive level columns) take their 11 source bytes
+        // from four LDS dwords: byte-align to the first byte, then one v_dot4 per output with
+        // weights (1,4,6,4) plus the fifth tap; quads that touch the reflect-101 border or
+        // the outside of the level take the per-column path.
+        static_assert(PV_W % 4 == 0, "pyrDown column quads");
+        constexpr int PQ = PV_W / 4;
+        uint2* HS2 = HSw;
+        for (int e = tid; e < nsr * PQ; e += 256) {
+            const int r = e / PQ, cq = e - r * PQ;
+            const int x0 = xc[4 * cq], x3 = xc[4 * cq + 3];
+            uint32_t o[4];
+            if (x0 >= 0 && x3 == x0 + 3 && xc[4 * cq + 1] == x0 + 1 && xc[4 * cq + 2] == x0 + 2) {
+                const int ob = r * PS_W + sh + (2 * x0 - 2 - sx0);
+                const uint32_t* wp = SRw + (ob >> 2);
+                const uint32_t sa = (uint32_t)(ob & 3);
+                const uint32_t W0 = wp[0], W1 = wp[1], W2 = wp[2], W3 = wp[3];
+                const uint32_t T0 = __builtin_amdgcn_alignbyte(W1, W0, sa);     // source bytes 0..3
+                const uint32_t T1 = __builtin_amdgcn_alignbyte(W2, W1, sa);     // 4..7
+                const uint32_t T2 = __builtin_amdgcn_alignbyte(W3, W2, sa);     // 8..11
+                constexpr uint32_t K4 = 0x04060401u;                            // taps 1,4,6,4
+                o[0] = __builtin_amdgcn_udot4(T0, K4, T1 & 0xffu, false);
+                o[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(T1, T0, 2), K4, (T1 >> 16) & 0xffu, false);
+                o[2] = __builtin_amdgcn_udot4(T1, K4, T2 & 0xffu, false);
+                o[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(T2, T1, 2), K4, (T2 >> 16) & 0xffu, false);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int x = xc[4 * cq + i];
+                    o[i] = 0;
+                    if (x >= 0) {
+                        const uint8_t* q = SR + r * PS_W + sh + (2 * x - 2 - sx0);
+                        o[i] = q[0] + 4 * q[1] + 6 * q[2] + 4 * q[3] + q[4];
+                    }
+                }
             }
-            HS[r * PV_W + c] = v;
+            HS2[r * PQ + cq] = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
         }
         __syncthreads();
-        for (int e = tid; e < PH * PV_W; e += 256) {
-            const int k = e / PV_W, c = e - k * PV_W;
+        // vertical [1 4 6 4 1] + (acc + 128) >> 8 on packed column pairs: a horizontal sum is
+        // <= 16 * 255 and a vertical one <= 65280, so the two 16-bit halves never carry into
+        // each other (columns outside the level hold 0 and give 0)
+        const uint2* HSq = HSw;
+        for (int e = tid; e < PH * PQ; e += 256) {
+            const int k = e / PQ, cq = e - k * PQ;
             const int y = yk[k];
-            uint8_t v = 0;
-            if (y >= 0 && xc[c] >= 0) {
-                const uint16_t* q = HS + (2 * y - 2 - sy0) * PV_W + c;
-                const int acc = q[0] + 4 * q[PV_W] + 6 * q[2 * PV_W] + 4 * q[3 * PV_W] + q[4 * PV_W];
-                v = (uint8_t)((acc + 128) >> 8);
+            uint32_t v = 0;
+            if (y >= 0) {
+                const uint2* q = HSq + (2 * y - 2 - sy0) * PQ + cq;
+                const uint2 q0 = q[0], q1 = q[PQ], q2 = q[2 * PQ], q3 = q[3 * PQ], q4 = q[4 * PQ];
+                const uint32_t ax = q0.x + 4 * q1.x + 6 * q2.x + 4 * q3.x + q4.x + 0x00800080u;
+                const uint32_t ay = q0.y + 4 * q1.y + 6 * q2.y + 4 * q3.y + q4.y + 0x00800080u;
+                // bytes (ax >> 8), (ax >> 24), (ay >> 8), (ay >> 24)
+                v = __builtin_amdgcn_perm(ay, ax, 0x07050301u);
             }
-            PV[e] = v;
+            PVw[k * (PV_W / 4) + cq] = v;
         }
-    }
-    __syncthreads();
+    }    __syncthreads();
     // 4 pixels x RPT rows per thread: pyramid dword stores, then the Scharr of interior pixels
     const int tc = tid & 31, tr = tid >> 5;
     const int px = px0 + 4 * tc;

@@ -202,7 +202,7 @@ class Engine:
         if os.environ.get("VO_ONE_STREAM") == "1":      # profiling: every stage on the main stream
             return torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
+            self._side = torch.cuda.Stream(self.device, priority=getattr(self, "side_priority", 0))
         return self._side
 
     def _step_launch(self, frames, prev, marks=None):
