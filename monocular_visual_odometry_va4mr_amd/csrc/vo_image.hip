@@ -2068,8 +2068,13 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
             dim3 g((pw + PT_W - 1) / PT_W, (ph + PYR0_TH - 1) / PYR0_TH, d->B);
             hipLaunchKernelGGL((k_pyr_level<true, PYR0_TH>), g, dim3(256), 0, VO_STREAM(stream), A);
         } else {
-            dim3 g((pw + PT_W - 1) / PT_W, (ph + PT_H - 1) / PT_H, d->B);
-            hipLaunchKernelGGL((k_pyr_level<false, PT_H>), g, dim3(256), 0, VO_STREAM(stream), A);
+            // tile rows of the pyrDown levels (VO_PYR_TH1 = 8 / 16 / 32 for experiments)
+            static const int th1 = [] { const char* e = getenv("VO_PYR_TH1"); return e ? atoi(e) : PT_H; }();
+            const int th = (th1 == 8 || th1 == 32) ? th1 : 16;
+            dim3 g((pw + PT_W - 1) / PT_W, (ph + th - 1) / th, d->B);
+            if (th == 8) hipLaunchKernelGGL((k_pyr_level<false, 8>), g, dim3(256), 0, VO_STREAM(stream), A);
+            else if (th == 32) hipLaunchKernelGGL((k_pyr_level<false, 32>), g, dim3(256), 0, VO_STREAM(stream), A);
+            else hipLaunchKernelGGL((k_pyr_level<false, 16>), g, dim3(256), 0, VO_STREAM(stream), A);
         }
     }
     return hip_ok() ? VO_OK : VO_EHIP;
