@@ -436,7 +436,7 @@ def main():
         "pyr_build": pyr_bytes(eng),
     }
     # the roofline row is the dominant kernel of the step: k_lk_w (track) has the largest
-    # kernel time per step in profiles/r1_summary.md (rocprofv3 --stats of this workload);
+    # kernel time per step in profiles/r1f_by_grid.csv (rocprofv3 trace of this workload);
     # stage event spans of the latency-bound gftt select / PnP stretch under the 2-stream overlap
     dom = "track"
     dom_ms = float(st_ms[names.index(dom)])

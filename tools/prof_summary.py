@@ -49,6 +49,18 @@ def pmc_avg(d, counter):
     return {k: v[0] / v[1] for k, v in acc.items() if v[1]}
 
 
+def pmc_calls(d, counter):
+    """launches per kernel in a --pmc pass (the per-step launch count comes from the PMC run,
+    whose command may differ from the stats pass)"""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    n = defaultdict(int)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == counter:
+                n[short(r["Kernel_Name"])] += 1
+    return n
+
+
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     chains = None
@@ -73,8 +85,10 @@ def main():
         w.writeheader()
         w.writerows(rows)
     fetch = write = {}
+    ncalls = {}
     if len(args) >= 4:
         fetch, write = pmc_avg(args[2], "FETCH_SIZE"), pmc_avg(args[3], "WRITE_SIZE")
+        ncalls = pmc_calls(args[2], "FETCH_SIZE")
     lines = [f"# rocprofv3 summary `{tag}`", "", "| kernel | calls | avg us | total ms | FETCH_SIZE x2 (MB/launch) | WRITE_SIZE (MB/launch) |",
              "|---|---:|---:|---:|---:|---:|"]
     traffic = {}
@@ -89,7 +103,7 @@ def main():
             st = STAGE_OF[k]
             e = traffic.setdefault(st, {"bytes_per_launch": 0.0, "kernels": {}, "chains": chains,
                                         "groups": groups, "tag": tag})
-            per_step = max(1, round(int(r["Calls"]) / (nsteps * groups))) if nsteps else 1
+            per_step = max(1, round(ncalls.get(k, 0) / (nsteps * groups))) if nsteps else 1
             b = (2 * fb * 1024 + wb * 1024) * per_step
             e["kernels"][k] = {"bytes_per_step": b, "launches_per_step": per_step}
             e["bytes_per_launch"] += b
