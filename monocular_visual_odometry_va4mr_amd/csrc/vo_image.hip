@@ -357,6 +357,9 @@ VO_DEV int to_sgpr(int v)
 {
     return __builtin_amdgcn_readfirstlane(v + opaque0());
 }
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+VO_DEV v2i16 as_v2i16(uint32_t u) { return __builtin_bit_cast(v2i16, u); }
+
 VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 {
     return (uint32_t)((w00 >> shift) & mask) | ((uint32_t)((w01 >> shift) & mask) << 8) |
@@ -819,6 +822,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const int iw11 = (1 << 14) - iw00 - iw01 - iw10;
                 int ival[MAXJ], ixv[MAXJ], iyv[MAXJ];
                 int a11 = 0, a12 = 0, a22 = 0;
+                // dI taps as int16 pairs against packed int16 weight pairs: two v_dot2_i32_i16
+                // per sum (exact: |dI| <= 4080, weights <= 2^14)
+                const v2i16 wp0 = as_v2i16((uint32_t)(iw00 & 0xffff) | ((uint32_t)iw01 << 16));
+                const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
                     const uint8_t* s = ir8 + toff[j] + ish;
@@ -826,10 +833,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
                     const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
                                           __mul24((int)s[QS], iw10) + __mul24((int)s[QS + 1], iw11), 9);
-                    const int gx2 = DESCALE(__mul24((int)(int16_t)d00, iw00) + __mul24((int)(int16_t)d01, iw01) +
-                                            __mul24((int)(int16_t)d10, iw10) + __mul24((int)(int16_t)d11, iw11), 14);
-                    const int gy2 = DESCALE(__mul24((int)(int16_t)(d00 >> 16), iw00) + __mul24((int)(int16_t)(d01 >> 16), iw01) +
-                                            __mul24((int)(int16_t)(d10 >> 16), iw10) + __mul24((int)(int16_t)(d11 >> 16), iw11), 14);
+                    const int gx2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x05040100u)), wp1,
+                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x05040100u)), wp0,
+                                                               1 << 13, false), false) >> 14;
+                    const int gy2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x07060302u)), wp1,
+                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x07060302u)), wp0,
+                                                               1 << 13, false), false) >> 14;
                     ival[j] = live[j] ? v : 0;
                     ixv[j] = live[j] ? gx2 : 0;
                     iyv[j] = live[j] ? gy2 : 0;
