@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stagger", type=int, default=0, help="1: start the groups out of phase (see main)")
     ap.add_argument("--prio", default="none", choices=["none", "g0", "side"], help="HIP stream priorities of the groups")
     ap.add_argument("--cpu-threads", type=int, default=16, help="chains in the multi-thread CPU leg (1: skip)")
     ap.add_argument("--cpu-mt-frames", type=int, default=30, help="steps per chain in the multi-thread CPU leg")
@@ -375,8 +376,27 @@ def main():
             with torch.cuda.stream(streams[g]):
                 e.step(frames[j, bounds[g]:bounds[g + 1]], marks=marks if g == 0 else None)
 
+    # --stagger: group g starts its first step only when group g-1's first `track` stage has
+    # ended, so the groups run out of phase: one group's latency-bound stages (PnP, select,
+    # triangulate) overlap another group's bulk stages (pyramid, LK, eig3) instead of all
+    # groups reaching their latency-bound stages together
     for i in range(W_steps):
-        step_all(2 + i)
+        if i == 0 and args.stagger and G > 1:
+            tr = Engine.STAGES.index("track")
+            prev_ev = None
+            for g, e in enumerate(engines):
+                if prev_ev is not None:
+                    streams[g].wait_event(prev_ev)
+                ev_g = torch.cuda.Event()
+
+                def mark(si, end, strm, ev_g=ev_g):
+                    if si == tr and end:
+                        ev_g.record(strm)
+                with torch.cuda.stream(streams[g]):
+                    e.step(frames[2 + i, bounds[g]:bounds[g + 1]], marks=mark)
+                prev_ev = ev_g
+        else:
+            step_all(2 + i)
     torch.cuda.synchronize()
 
     nst = len(Engine.STAGES)
