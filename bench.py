@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=384, help="chains (shards) per GPU")
+    ap.add_argument("--chains", type=int, default=768, help="chains (shards) per GPU")
     ap.add_argument("--groups", type=int, default=2,
                     help="split the chains into this many engines, each on its own HIP stream "
                          "(latency-bound stages of one group overlap the others' kernels)")
