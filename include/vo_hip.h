@@ -69,7 +69,8 @@ typedef struct vo_opts {
     double K[9], K_inv[9];
     double min_dist_landmarks, max_dist_landmarks;
     double min_baseline_angle;    /* degrees                                            */
-    double cos_baseline;          /* cos(radians(min_baseline_angle)), host-computed    */
+    double cos_baseline;          /* smallest c with degrees(arccos(c)) < min_baseline_angle
+                                     under the host's numpy (exact gate, :144-147); 2 = never */
     int32_t min_baseline_frames;
     double feature_ratio;
     int32_t feature_max_corners;

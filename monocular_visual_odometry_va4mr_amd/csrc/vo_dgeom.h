@@ -3,9 +3,10 @@
 // Rodrigues, Sampson error.  Each routine follows the operation order of its CPU
 // oracle counterpart in oracle/vo_oracle_geom.c (which restates OpenCV 4.6, SURVEY.md
 // Appendix A) so that, compiled with -ffp-contract=off, results agree bit for bit
-// except where a libm transcendental (acos/sin/cos/log/pow) is involved.
+// (the libm transcendentals acos/sin/cos/log/pow come from vo_crmath.h on both sides).
 #pragma once
 #include "vo_dev.h"
+#include "vo_crmath.h"
 
 #include <float.h>
 
@@ -342,7 +343,7 @@ VO_DEV void rodrigues_v2m(const double* r, double* R)
         for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
         return;
     }
-    double c = cos(th), s = sin(th), c1 = 1.0 - c, it = th ? 1.0 / th : 0.0;
+    double c = vcr_cos(th), s = vcr_sin(th), c1 = 1.0 - c, it = th ? 1.0 / th : 0.0;
     double x = r[0] * it, y = r[1] * it, z = r[2] * it;
     double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
     double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
@@ -361,7 +362,7 @@ VO_DEV void rodrigues_m2v(const double* Rin, double* rv)
     double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
-    double th = acos(c);
+    double th = vcr_acos(c);
     if (s < 1e-5) {
         if (c > 0) { rx = ry = rz = 0; }
         else {
@@ -728,10 +729,10 @@ VO_DEV int ransac_update_niters(double p, double ep, int model_points, int max_i
     p = p < 0 ? 0 : (p > 1 ? 1 : p);
     ep = ep < 0 ? 0 : (ep > 1 ? 1 : ep);
     double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-    double denom = 1. - pow(1. - ep, (double)model_points);
+    double denom = 1. - vcr_powi(1. - ep, model_points);
     if (denom < DBL_MIN) return 0;
-    num = log(num);
-    denom = log(denom);
+    num = vcr_log(num);
+    denom = vcr_log(denom);
     return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
 }
 

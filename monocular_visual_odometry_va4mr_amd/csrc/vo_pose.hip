@@ -656,7 +656,11 @@ __global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const 
         const double* t = tvec + 3 * b;
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) Rcw[i * 3 + j] = Rwc[j * 3 + i];
-        for (int i = 0; i < 3; ++i) tcw[i] = -(Rcw[i * 3] * t[0] + Rcw[i * 3 + 1] * t[1] + Rcw[i * 3 + 2] * t[2]);
+        // invert_transform :74-75, tnew = -Rnew @ t with Rnew = R.T: numpy hands the (column-
+        // major) matrix to BLAS gemv, which accumulates the columns j = 0, 1, 2 with fused
+        // multiply-adds -- reproduced here so the pose is bit-identical (tools/blas_order_probe.py)
+        for (int i = 0; i < 3; ++i)
+            tcw[i] = __builtin_fma(-Rcw[i * 3 + 2], t[2], __builtin_fma(-Rcw[i * 3 + 1], t[1], -Rcw[i * 3] * t[0]));
     }
 }
 
@@ -665,7 +669,8 @@ struct TriArgs {
     vo_dims d;
     vo_state s;
     double K[9], Kinv[9];
-    double min_d, max_d, min_angle;
+    double min_d, max_d;
+    double cos_thr;        // retain iff clip(cos) >= cos_thr  <=>  degrees(arccos(cos)) < min_baseline_angle
     int min_frames;
     int force;
 };
@@ -733,8 +738,10 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
                 double np = sqrt(vp[0] * vp[0] + vp[1] * vp[1] + vp[2] * vp[2]);
                 double cs = dot / (nc * np);
                 cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
-                const double ang = acos(cs) * 57.29577951308232;      // np.degrees(np.arccos(.))
-                if (ang < A.min_angle) {
+                // np.degrees(np.arccos(c)) < min_baseline_angle (:144-147) without a device acos:
+                // arccos is monotone, so the gate is c >= the smallest double the host's own
+                // np.arccos puts inside the angle (engine.baseline_cos_threshold); NaN stays false
+                if (cs >= A.cos_thr) {
                     retain = true;
                 } else {
                     double Rpw[9], tpw[3], Pp[12];
@@ -980,7 +987,7 @@ extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state
     for (int i = 0; i < 9; ++i) { A.K[i] = o->K[i]; A.Kinv[i] = o->K_inv[i]; }
     A.min_d = o->min_dist_landmarks;
     A.max_d = o->max_dist_landmarks;
-    A.min_angle = o->min_baseline_angle;
+    A.cos_thr = o->cos_baseline;
     A.min_frames = o->min_baseline_frames;
     A.force = force;
     hipLaunchKernelGGL(k_triangulate, dim3(d->B), dim3(256), 0, VO_STREAM(stream), A);

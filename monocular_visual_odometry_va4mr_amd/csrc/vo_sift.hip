@@ -10,6 +10,7 @@
 // SIFT descriptor entries are integers 0..255 (exact in bf16) and sums stay below 2^24,
 // so distances are exact; the per-query top-2 scan keeps OpenCV's tie order.
 #include "vo_dev.h"
+#include "vo_crmath.h"
 
 #include <stdlib.h>
 
@@ -269,7 +270,7 @@ VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, KP& kpt, int octv, int& 
     kpt.x = ((float)c + xc) * (float)(1 << octv);
     kpt.y = ((float)r + xr) * (float)(1 << octv);
     kpt.octave = octv + (layer << 8) + ((int)rint((xi + 0.5) * 255) << 16);
-    kpt.size = sigma * (float)pow(2.0, (double)(((float)layer + xi) / N_LAYERS)) * (float)(1 << octv) * 2;
+    kpt.size = sigma * (float)vcr_exp2((double)(((float)layer + xi) / N_LAYERS)) * (float)(1 << octv) * 2;
     kpt.response = fabsf(contr);
     return true;
 }
@@ -582,8 +583,8 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
     const float ori = angle, scl = size * 0.5f;
     const int d = 4, n = 8;
     const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
-    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180)));
-    float sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
+    float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
     const float bins_per_rad = n / 360.f;
     const float exp_scale = -1.f / (d * d * 0.5f);
     const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
@@ -701,8 +702,8 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
     const float ori = angle, scl = size * 0.5f;
     const int d = 4, n = 8;
     const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
-    float cos_t = (float)cos((double)(ori * (float)(M_PI / 180)));
-    float sin_t = (float)sin((double)(ori * (float)(M_PI / 180)));
+    float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
+    float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
     const float bins_per_rad = n / 360.f;
     const float exp_scale = -1.f / (d * d * 0.5f);
     const float hist_width = SIFT_DESCR_SCL_FCTR * scl;

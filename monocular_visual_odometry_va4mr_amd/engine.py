@@ -19,7 +19,6 @@ and runtime ValueErrors of the reference become per-chain status codes (``status
 from __future__ import annotations
 
 import ctypes as C
-import math
 
 import os
 
@@ -39,6 +38,41 @@ def pyr_max_level(w: int, h: int, win=(15, 15), max_level: int = 3) -> int:
     return max_level
 
 
+def _f64_key(x: float) -> int:
+    """Order-preserving integer image of a double (for bisection over representable values)."""
+    i = int(np.array([x], np.float64).view(np.int64)[0])
+    return i if i >= 0 else -(i & 0x7FFFFFFFFFFFFFFF)
+
+
+def _f64_from_key(k: int) -> float:
+    i = k if k >= 0 else (-k) | -0x8000000000000000
+    return float(np.array([i], np.int64).view(np.float64)[0])
+
+
+def baseline_cos_threshold(min_angle_deg: float) -> float:
+    """The baseline-angle gate of check_baseline (VisualOdometryPipeLine.py:144-147),
+    ``np.degrees(np.arccos(np.clip(c, -1, 1))) < min_baseline_angle``, as a threshold on c.
+
+    arccos is monotone, so the gate holds exactly for c >= the smallest double c* for which
+    the expression is true *as this host's numpy evaluates it* (same 1-element array path as
+    the reference).  The kernel then compares c >= c*, with no device acos; the two agree for
+    every double c (and both are false for NaN).  Returns 2.0 when no c passes."""
+    def gate(c: float) -> bool:
+        return bool(np.degrees(np.arccos(np.array([c], np.float64)))[0] < min_angle_deg)
+    if not gate(1.0):
+        return 2.0
+    if gate(-1.0):
+        return -1.0
+    lo, hi = _f64_key(-1.0), _f64_key(1.0)         # gate(lo) false, gate(hi) true
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if gate(_f64_from_key(mid)):
+            hi = mid
+        else:
+            lo = mid
+    return _f64_from_key(hi)
+
+
 def make_opts(K: np.ndarray, options: dict) -> L.VoOpts:
     o = L.VoOpts()
     K = np.asarray(K, np.float64)
@@ -49,7 +83,7 @@ def make_opts(K: np.ndarray, options: dict) -> L.VoOpts:
     o.min_dist_landmarks = float(options["min_dist_landmarks"])
     o.max_dist_landmarks = float(options["max_dist_landmarks"])
     o.min_baseline_angle = float(options["min_baseline_angle"])
-    o.cos_baseline = math.cos(math.radians(float(options["min_baseline_angle"])))
+    o.cos_baseline = baseline_cos_threshold(float(options["min_baseline_angle"]))
     o.min_baseline_frames = int(options["min_baseline_frames"])
     o.feature_ratio = float(options.get("feature_ratio", 0.8))
     o.feature_max_corners = int(options["feature_max_corners"])

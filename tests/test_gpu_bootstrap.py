@@ -74,19 +74,21 @@ def test_bf_knn2_batch_exact():
     assert big > 0          # the fixup path ran
 
 
-def test_sift_matches_oracle():
+@pytest.mark.parametrize("preset,seed", [("parking", 4), ("kitti", 1), ("malaga1024", 2), ("hd1080", 3)])
+def test_sift_matches_oracle(preset, seed):
+    """detectAndCompute (:226-227) bit for bit against the C restatement at every BASELINE
+    image size: C1 640x480, C2 1241x376, C3 1024x768, C5 1920x1080 -- keypoint order,
+    x, y, size, angle, response, octave and all 128 descriptor bins."""
     from oracle import _olib as O
     from monocular_visual_odometry_va4mr_amd import cv2compat as G
     from monocular_visual_odometry_va4mr_amd.synth import make_sequence
-    fr, _, _, _ = make_sequence("parking", 1, seed=4)
+    fr, _, _, _ = make_sequence(preset, 1, seed=seed)
     kps, desc = G.SIFT_create().detectAndCompute(fr[0], None)
     ko, do = O.sift(fr[0])
     kg = np.array([[k.pt[0], k.pt[1], k.size, k.angle, k.response, k.octave] for k in kps], np.float32)
-    assert len(kg) == len(ko)
-    assert np.abs(kg[:, :5] - ko[:, :5]).max() <= 1e-4 * np.abs(ko[:, :5]).max()
-    assert np.array_equal(kg[:, 5], ko[:, 5])
-    diff = np.abs(desc - do)
-    assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
+    assert len(kg) == len(ko) > 300
+    assert np.array_equal(kg, ko)
+    assert np.array_equal(desc, do)
 
 
 def test_sift_desc_wave_equals_serial(monkeypatch):
@@ -152,7 +154,7 @@ def _oracle_init(case):
     return g, fr, opts, boot, s
 
 
-@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1"])
+@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3"])
 def test_bootstrap_matches_oracle(case):
     from monocular_visual_odometry_va4mr_amd.VisualOdometryPipeLine import VisualOdometryPipeLine
     g, fr, opts, boot, s = _oracle_init(case)
@@ -161,14 +163,22 @@ def test_bootstrap_matches_oracle(case):
     assert vo.num_pts == [int(s.num_pts[0])]
     R_g, t_g = vo.transforms[-1]
     R_o, t_o = s.transforms[-1]
-    assert np.abs(R_g - R_o).max() < 1e-6 and np.abs(t_g - t_o).max() < 1e-6
-    assert abs(len(vo.matched_landmarks) - len(s.lm)) <= 2
-    assert abs(len(vo.potential_keys) - len(s.cand)) <= 2
+    assert np.array_equal(R_g, R_o) and np.array_equal(t_g, t_o)
+    assert np.array_equal(vo.matched_landmarks, s.lm)
+    assert np.array_equal(vo.matched_keypoints, s.kp)
+    assert np.array_equal(vo.potential_keys, s.cand)
+    assert np.array_equal(vo.potential_first_keys, s.cand_first)
+    assert np.array_equal(vo.potential_transforms, s.cand_tau)
+    assert np.array_equal(vo.inlier_pts_current, s.inl_pts)
+    assert np.array_equal(vo.outlier_pts_current, s.outl_pts)
 
 
 @pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3"])
 def test_full_pipeline_ate_vs_reference(case):
-    """Drop-in class on GPU vs the reference class's own trajectory (golden fixture)."""
+    """Drop-in class on GPU vs the reference class's own run (golden fixture, produced by
+    /root/reference/VisualOdometryPipeLine.py on the oracle primitives): every pose, every
+    num_pts / landmark / candidate count and the snapshot arrays are bit-identical; the
+    ATE (Umeyama Sim(3), reported) is therefore 0."""
     from conftest import golden_frames, load_golden
     from monocular_visual_odometry_va4mr_amd import options as Op
     from monocular_visual_odometry_va4mr_amd.VisualOdometryPipeLine import VisualOdometryPipeLine
@@ -176,14 +186,24 @@ def test_full_pipeline_ate_vs_reference(case):
     g = load_golden(case)
     fr = golden_frames(g)
     opts, boot, _ = Op.get(str(g["preset"]))
-    vo = VisualOdometryPipeLine(g["K"], opts, max_frames=256, landmark_capacity=4096, candidate_capacity=8192)
+    n = len(g["frame"])
+    vo = VisualOdometryPipeLine(g["K"], opts, max_frames=max(256, n + 8), landmark_capacity=8192,
+                                candidate_capacity=16384)
     vo.initialization(fr[boot[0]], fr[boot[1]])
+    counts = [(len(vo.matched_landmarks), len(vo.potential_keys))]
     for i in g["frame"][1:]:
         vo.continuous_operation(fr[i])
-    est = np.array([t.ravel() for _, t in vo.transforms[1:]])
-    ref = g["t"][:, :, 0]
-    assert len(est) == len(ref)
-    rmse, rel = ate(est, ref)
-    assert rel < 0.01, f"ATE {rmse:.4f} = {100 * rel:.3f}% of path length"
-    n_ok = np.mean(np.abs(np.array(vo.num_pts) - g["num_pts"]) <= 0.05 * g["num_pts"] + 2)
-    assert n_ok > 0.8
+        counts.append((len(vo.matched_landmarks), len(vo.potential_keys)))
+        if f"lm_{i}" in g:
+            assert np.array_equal(vo.matched_landmarks, g[f"lm_{i}"]), f"landmarks at frame {i}"
+            assert np.array_equal(vo.potential_keys, g[f"cand_{i}"]), f"candidates at frame {i}"
+            assert np.array_equal(vo.potential_transforms, g[f"cand_tau_{i}"]), f"frame indices at {i}"
+    tr = vo.transforms[1:]
+    assert len(tr) == len(g["t"])
+    assert np.array_equal(np.stack([R for R, _ in tr]), g["R"])
+    assert np.array_equal(np.stack([t for _, t in tr]), g["t"])
+    assert vo.num_pts == [int(v) for v in g["num_pts"]]
+    assert np.array_equal(np.array(counts), np.stack([g["N"], g["P"]], 1))
+    est = np.array([t.ravel() for _, t in tr])
+    rmse, rel = ate(est, g["t"][:, :, 0])
+    assert rel == 0.0 or rel < 1e-12
