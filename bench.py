@@ -13,8 +13,9 @@ continuous_operation (VisualOdometryPipeLine.py:326-373) on the following frames
 frames are rendered into HBM before the timed region.
 
 A "step" = one continuous_operation of every chain on its rank (B frames per GPU).  Timed
-region: K steps between barrier + device synchronisation; value = frames of all ranks /
-max-over-ranks time (weak scaling: B chains per GPU whatever N is).
+region: K steps between barrier + device synchronisation; value = frames of the chains of
+all ranks that are still tracking (status 0) after the timed region / max-over-ranks time
+(weak scaling: B chains per GPU whatever N is).
 
 Extra JSON fields:
   roofline     -- the dominant stage, timed with HIP events recorded on the engine's
@@ -414,10 +415,18 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t_start
 
+    # chains still tracking (status 0) after the timed region: only their frames count; a
+    # chain that fails returns early from every kernel and produces no poses
+    statuses = np.concatenate([e.statuses() for e in engines])
+    n_ok = int((statuses == 0).sum())
+    n_ok_all = n_ok
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        ok_t = torch.tensor([n_ok], dtype=torch.int64, device=device)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.SUM)
+        n_ok_all = int(ok_t.item())
 
     # per-stage HIP-event times (ms) of group 0 (events on its stream), mean over timed steps
     st_ms = np.zeros(nst)
@@ -430,8 +439,6 @@ def main():
     npts = int((eng.t["nL"].to(torch.int64) + eng.t["nC"].to(torch.int64)).sum())
     ncor = int(eng.t["nCorners"].to(torch.int64).sum())
     gf_pass = eng.t["gf_n"].to(torch.float64)
-    statuses = np.concatenate([e.statuses() for e in engines])
-    n_ok = int((statuses == 0).sum())
 
     # final pose gather to rank 0 (the one collective of the sharded path, §8e)
     t_g = time.perf_counter()
@@ -446,7 +453,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    frames_total = world * B * K_steps
+    frames_total = n_ok_all * K_steps          # frames of chains that tracked through the timed region
     value = frames_total / elapsed
     names = list(Engine.STAGES)
     stage = {n: round(float(m), 4) for n, m in zip(names, st_ms)}
@@ -495,7 +502,9 @@ def main():
                    "seed": args.seed},
         "roofline": roof,
         "stages_ms": stage,
-        "chains_ok": n_ok,
+        "chains_ok": n_ok_all,
+        "chains_failed": world * B - n_ok_all,
+        "frames_counted": frames_total,
         "chain_status": {str(int(k)): int(v) for k, v in zip(*np.unique(statuses, return_counts=True))},
         "points_last_step": npts,
         "gftt_candidates_mean": round(float(gf_pass.mean()), 1),

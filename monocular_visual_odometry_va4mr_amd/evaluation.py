@@ -67,21 +67,43 @@ def rpe(est: np.ndarray, ref: np.ndarray, delta: int = 1):
     return float(np.sqrt(np.mean(np.square(te)))), float(np.sqrt(np.mean(np.square(re))))
 
 
-def shard_report(shards, centres, gt_positions, stitched=None) -> dict:
-    """ATE of every shard against ground truth over its own frames, and of the stitched
-    trajectory over all frames it covers."""
+def shard_report(shards, centres, gt_positions, stitched=None, reference=None) -> dict:
+    """ATE of every shard against ground truth over its own frames (and, when ``reference``
+    maps shard index -> the reference CPU path's positions on the same shard boundaries,
+    against those: SURVEY.md §8e's parity definition), and of the stitched trajectory over
+    the frames it covers.  A stitched result with coverage breaks is evaluated per segment
+    (each segment Sim(3)-aligned on its own); the breaks are listed."""
     gt = np.asarray(gt_positions, np.float64)
     per = []
     for s, c in zip(shards, centres):
         fr = np.array([s.start] + list(range(s.boot1, s.end)))[:len(c)]
         if len(fr) >= 3:
             rmse, rel = ate(np.asarray(c)[:len(fr)], gt[fr])
-            per.append({"shard": s.index, "frames": int(len(fr)), "ate_rmse": rmse, "ate_rel": rel})
+            rec = {"shard": s.index, "frames": int(len(fr)), "ate_rmse": rmse, "ate_rel": rel}
+            if reference is not None and s.index in reference:
+                r = np.asarray(reference[s.index], np.float64)
+                m = min(len(r), len(c))
+                rec["ref_frames"] = int(m)
+                rec["identical_to_ref"] = bool(len(r) == len(c) and np.array_equal(np.asarray(c), r))
+                if m >= 3:
+                    rr, rl = ate(np.asarray(c)[:m], r[:m])
+                    rec["ate_vs_ref_rmse"], rec["ate_vs_ref_rel"] = rr, rl
+            per.append(rec)
     out = {"shards": per}
     if stitched is not None:
-        keep = ~np.isnan(stitched[:, 0])
-        n = min(len(stitched), len(gt))
-        keep = keep[:n]
-        rmse, rel = ate(stitched[:n][keep], gt[:n][keep])
-        out["stitched"] = {"frames": int(keep.sum()), "ate_rmse": rmse, "ate_rel": rel}
+        pos = stitched.positions
+        n = min(len(pos), len(gt))
+        segs = []
+        for k in range(len(stitched.segments)):
+            keep = stitched.segment[:n] == k
+            if keep.sum() >= 3:
+                rmse, rel = ate(pos[:n][keep], gt[:n][keep])
+                segs.append({"shards": list(stitched.segments[k]), "frames": int(keep.sum()),
+                             "ate_rmse": rmse, "ate_rel": rel})
+        covered = int((stitched.segment[:n] >= 0).sum())
+        out["stitched"] = {"frames": covered, "segments": segs,
+                           "coverage_breaks": [list(b) for b in stitched.breaks]}
+        if len(segs) == 1:
+            out["stitched"]["ate_rmse"] = segs[0]["ate_rmse"]
+            out["stitched"]["ate_rel"] = segs[0]["ate_rel"]
     return out

@@ -8,10 +8,12 @@
 The sequence is cut into N*B contiguous shards with overlap (shards.plan_shards); rank r
 owns a block of B shards and runs them as the B chains of one Engine: bootstrap at
 [s, s+gap] (main.py:18,48,78), then continuous_operation on the following frames, feeding
-every chain its own next frame each step.  When all ranks are done, the per-chain poses are
-all-gathered to rank 0 (the one collective; RCCL on GPUs), which stitches the shards with
-Sim(3) fits on the overlap frames and evaluates against ground truth.  Frames come from the
-seeded renderer (synth.py), rendered on the GPU per step.
+every chain its own next frame each step.  When all ranks are done, the per-chain poses and
+statuses are all-gathered to rank 0 (the one collective; RCCL on GPUs), which stitches the
+surviving shards with Sim(3) fits on the overlap frames (a shard that cannot be chained opens
+a new segment and is reported as a coverage break) and evaluates against ground truth and,
+when given, against the reference CPU path's per-shard trajectories (§8e parity).  Frames
+come from the seeded renderer (synth.py), rendered on the device per step.
 """
 from __future__ import annotations
 
@@ -26,83 +28,131 @@ import torch
 from . import evaluation as Ev
 from . import options as Op
 from . import shards as Sh
-from .engine import Engine
-from .synth import Renderer, poses
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, seed: int = 1, device=None,
-        rank: int = 0, world: int = 1, out_path: str | None = None) -> dict | None:
+        rank: int = 0, world: int = 1, out_path: str | None = None, engine_cls=None, renderer=None,
+        reference: dict | None = None) -> dict | None:
+    """Run the plan; rank 0 returns the report (None on other ranks).
+
+    ``engine_cls`` / ``renderer`` default to engine.Engine and synth.Renderer (tests pass
+    stand-ins to exercise the cross-rank bookkeeping on CPU); ``reference`` maps a global
+    shard index to the reference CPU trajectory of that shard (positions [n, 3])."""
     dev = torch.device(device or "cuda")
+    if engine_cls is None:
+        from .engine import Engine as engine_cls
+    if renderer is None:
+        from .synth import Renderer
+        renderer = Renderer(preset, seed=seed, device=dev)
+    from .synth import poses
     opts, (b0, b1), _ = Op.get(preset)
     gap = b1 - b0
     plan = Sh.plan_shards(n_frames, world * shards_per_rank, gap, overlap)
     mine = Sh.rank_shards(plan, rank, world)
     B = len(mine)
-    rend = Renderer(preset, seed=seed, device=dev)
-    Rs, cs = poses(n_frames, rend.p)
+    Rs, cs = poses(n_frames, renderer.p)
     max_f = max(s.end - s.boot1 + 1 for s in plan)
-    eng = Engine(rend.K, opts, rend.W, rend.H, batch=B, device=dev, ncap=16384, pcap=16384, fcap=max_f + 8)
+    eng = engine_cls(renderer.K, opts, renderer.W, renderer.H, batch=B, device=dev, ncap=16384, pcap=16384,
+                     fcap=max_f + 8)
 
     def frames_at(ids):
         ids = [min(int(i), n_frames - 1) for i in ids]
-        return rend.render_batch(ids, Rs[ids], cs[ids])
+        return renderer.render_batch(ids, Rs[ids], cs[ids])
 
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t0 = time.perf_counter()
     eng.bootstrap(frames_at([s.start for s in mine]), frames_at([s.boot1 for s in mine]))
+    _sync(dev)
+    t_boot = time.perf_counter() - t0
     n_steps = max(s.n_steps for s in mine)
+    # status of every chain at its shard's own last step (chains whose shard has ended keep
+    # re-reading their last frame until the longest shard is done; what happens to them then
+    # does not count).  Kept on the device: no host sync inside the loop.
+    last_step = torch.tensor([s.n_steps - 1 for s in mine], device=dev)
+    final_status = eng.t["status"].clone()
     t_step = 0.0
     for j in range(n_steps):
-        # chains whose shard has ended keep re-reading their last frame (zero motion);
-        # their extra poses are dropped below
         fr = frames_at([min(s.boot1 + 1 + j, s.end - 1) for s in mine])
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         ts = time.perf_counter()
         eng.step(fr)
-        torch.cuda.synchronize(dev)
+        _sync(dev)
         t_step += time.perf_counter() - ts
+        final_status = torch.where(last_step == j, eng.t["status"], final_status)
+    final_status = torch.where(last_step < 0, eng.t["status"], final_status)
     wall = time.perf_counter() - t0
     packed = Sh.pack_poses(eng.t["pose_R"], eng.t["pose_t"], eng.t["nF"], eng.dims.fcap)
     allp = Sh.gather_poses(packed)
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
-        st_all = [torch.empty_like(eng.t["status"]) for _ in range(world)]
-        dist.all_gather(st_all, eng.t["status"])
+        st_all = [torch.empty_like(final_status) for _ in range(world)]
+        dist.all_gather(st_all, final_status.contiguous())
         statuses = torch.cat(st_all).cpu().numpy()
-        tt = torch.tensor([t_step, wall], dtype=torch.float64, device=dev)
+        tt = torch.tensor([t_step, wall, t_boot], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step, wall = (float(v) for v in tt.cpu())
+        t_step, wall, t_boot = (float(v) for v in tt.cpu())
     else:
-        statuses = eng.t["status"].cpu().numpy()
+        statuses = final_status.cpu().numpy()
     if allp is None:
         return None
     allp = allp.cpu().numpy()
-    centres, ok_shards, ok_centres = [], [], []
-    for s, chain in zip(plan, allp):
-        c = Sh.unpack_centres(chain)[: s.end - s.boot1 + 1]
-        centres.append(c)
+    centres = [Sh.unpack_centres(chain)[: s.end - s.boot1 + 1] for s, chain in zip(plan, allp)]
+    ok_shards, ok_centres, failed = [], [], []
     for s, c, st in zip(plan, centres, statuses):
         if st == 0 and len(c) == s.end - s.boot1 + 1:
             ok_shards.append(s)
             ok_centres.append(c)
+        else:
+            failed.append({"shard": s.index, "status": int(st), "poses": int(len(c))})
     stitched = Sh.stitch(ok_shards, ok_centres) if ok_shards else None
-    rep = Ev.shard_report(ok_shards, ok_centres, cs, stitched)
+    rep = Ev.shard_report(ok_shards, ok_centres, cs, stitched, reference=reference)
     frames_done = sum(s.n_steps for s in plan)
+    per = rep["shards"]
     out = {
         "preset": preset, "frames": n_frames, "shards": len(plan), "gpus": world, "chains_per_gpu": shards_per_rank,
-        "overlap": overlap, "shards_ok": len(ok_shards),
+        "overlap": overlap, "shards_ok": len(ok_shards), "failed_shards": failed,
         "shard_status": {str(int(k)): int(v) for k, v in zip(*np.unique(statuses, return_counts=True))},
+        "sequence_frames_per_s": round(n_frames / max(wall, 1e-9), 1),
         "step_frames_per_s": round(frames_done / max(t_step, 1e-9), 1),
-        "wall_s": round(wall, 2), "step_s": round(t_step, 3),
-        "shard_ate_rel_max": max((p["ate_rel"] for p in rep["shards"]), default=None),
+        "wall_s": round(wall, 3), "bootstrap_s": round(t_boot, 3), "step_s": round(t_step, 3),
+        "shard_ate_rel_max": max((p["ate_rel"] for p in per), default=None),
         "stitched": rep.get("stitched"),
     }
+    if reference is not None:
+        vs = [p for p in per if "ref_frames" in p]
+        out["vs_reference"] = {
+            "shards_compared": len(vs),
+            "shards_identical": int(sum(p["identical_to_ref"] for p in vs)),
+            "ate_rel_max": max((p.get("ate_vs_ref_rel", 0.0) for p in vs), default=None),
+        }
     if out_path and stitched is not None:
-        keep = ~np.isnan(stitched[:, 0])
-        np.savetxt(out_path, np.c_[np.nonzero(keep)[0], stitched[keep]], fmt=["%d", "%.9f", "%.9f", "%.9f"])
+        keep = ~np.isnan(stitched.positions[:, 0])
+        np.savetxt(out_path, np.c_[np.nonzero(keep)[0], stitched.segment[keep], stitched.positions[keep]],
+                   fmt=["%d", "%d", "%.9f", "%.9f", "%.9f"])
     out["_centres"] = centres
     out["_plan"] = plan
+    out["_statuses"] = statuses
     return out
+
+
+def reference_shards(path: str, n_shards: int) -> dict | None:
+    """Per-shard reference CPU trajectories from tests/golden/kitti_seq00_shards.npz
+    (generated by the reference class on the same shard boundaries, make_long_golden.py)."""
+    if not os.path.exists(path):
+        return None
+    g = np.load(path, allow_pickle=False)
+    key = f"s{n_shards}_t"
+    if key not in g.files:
+        return None
+    t, off = g[key], g[f"s{n_shards}_off"]
+    # the fixture holds transforms[1:] (the bootstrap pose onwards); transforms[0] is the
+    # identity at the first bootstrap frame, as in the engine's pose list
+    return {k: np.concatenate([np.zeros((1, 3)), t[off[k]:off[k + 1]]]) for k in range(n_shards)}
 
 
 def main():
@@ -112,7 +162,8 @@ def main():
     ap.add_argument("--shards-per-gpu", type=int, default=8)
     ap.add_argument("--overlap", type=int, default=30)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--out", default=None, help="write the stitched positions (frame x y z)")
+    ap.add_argument("--reference", default=None, help="per-shard reference trajectories (.npz)")
+    ap.add_argument("--out", default=None, help="write the stitched positions (frame segment x y z)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -122,7 +173,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    res = run(args.preset, args.frames, args.shards_per_gpu, args.overlap, args.seed, dev, rank, world, args.out)
+    ref = reference_shards(args.reference, world * args.shards_per_gpu) if args.reference else None
+    res = run(args.preset, args.frames, args.shards_per_gpu, args.overlap, args.seed, dev, rank, world, args.out,
+              reference=ref)
     if res is not None:
         print(json.dumps({k: v for k, v in res.items() if not k.startswith("_")}))
     if world > 1:

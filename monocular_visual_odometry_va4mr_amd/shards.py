@@ -86,39 +86,63 @@ def unpack_centres(packed_chain: np.ndarray) -> np.ndarray:
     return packed_chain[valid, 9:12]
 
 
-def stitch(shards: list[Shard], centres: list[np.ndarray]) -> np.ndarray:
+@dataclass
+class Stitched:
+    """Result of ``stitch``.
+
+    positions  [total, 3] camera centres, NaN where no shard covers a frame; every segment
+               is expressed in the frame of its own first shard
+    segment    [total] segment id per frame (-1: not covered)
+    segments   shard indices of each segment, in chaining order
+    breaks     (previous shard, next shard, common frames) for every place where chaining
+               was impossible (< 3 overlapping frames, e.g. a failed shard in between): the
+               next shard starts a new segment instead of being placed at an arbitrary pose
+    """
+    positions: np.ndarray
+    segment: np.ndarray
+    segments: list
+    breaks: list
+
+
+def stitch(shards: list[Shard], centres: list[np.ndarray], min_common: int = 3) -> Stitched:
     """Chain per-shard trajectories into one: shard k+1 is mapped onto shard k's frame by
     the Sim(3) that aligns their overlapping camera centres (Umeyama), accumulated.
 
     ``centres[k]`` holds poses for frames [boot0] + [boot1 .. end) of shard k, as in
-    transforms (index 0 = identity at the first bootstrap frame).  Returns per-frame
-    positions for frames [0, last end), NaN where no shard covers a frame."""
-    if not shards:
-        return np.zeros((0, 3))
-    total = max(s.end for s in shards)
+    transforms (index 0 = identity at the first bootstrap frame).  A shard that shares fewer
+    than ``min_common`` frames with the previous surviving shard cannot be placed; it opens
+    a new segment and the break is reported (a failed shard is reported, not
+    silently stitched)."""
+    total = max((s.end for s in shards), default=0)
     out = np.full((total, 3), np.nan)
+    seg_of = np.full(total, -1, np.int64)
+    segments, breaks = [], []
 
     def frames_of(s: Shard):
         return np.array([s.start] + list(range(s.boot1, s.end)))
 
-    prev_map = None     # frame -> position in the global frame for the previous shard
+    prev_map = None     # frame -> position in the current segment's frame (previous shard)
+    prev_shard = None
     for s, c in zip(shards, centres):
         fr = frames_of(s)[:len(c)]
         c = np.asarray(c, np.float64)[:len(fr)]
-        if prev_map is None:
-            sc, R, t = 1.0, np.eye(3), np.zeros(3)
+        common = [] if prev_map is None else [i for i, f in enumerate(fr) if int(f) in prev_map]
+        if prev_map is not None and len(common) >= min_common:
+            src = c[common]
+            dst = np.array([prev_map[int(fr[i])] for i in common])
+            sc, R, t = umeyama(src, dst, True)
+            segments[-1].append(s.index)
         else:
-            common = [i for i, f in enumerate(fr) if f in prev_map]
-            if len(common) >= 3:
-                src = c[common]
-                dst = np.array([prev_map[fr[i]] for i in common])
-                sc, R, t = umeyama(src, dst, True)
-            else:
-                sc, R, t = 1.0, np.eye(3), np.zeros(3)
+            if prev_map is not None:
+                breaks.append((prev_shard, s.index, len(common)))
+            sc, R, t = 1.0, np.eye(3), np.zeros(3)
+            segments.append([s.index])
         g = (sc * (R @ c.T)).T + t
         prev_map = {}
         for f, p in zip(fr, g):
             prev_map[int(f)] = p
-            if np.isnan(out[f, 0]):
+            if seg_of[f] < 0:
                 out[f] = p
-    return out
+                seg_of[f] = len(segments) - 1
+        prev_shard = s.index
+    return Stitched(out, seg_of, segments, breaks)

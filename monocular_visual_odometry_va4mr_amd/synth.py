@@ -13,6 +13,13 @@ Scene: a textured "canyon" -- ground plane, two side walls and a ceiling -- whos
 texture is multi-octave value noise, band-limited per pixel by the world-space
 footprint so that far surfaces fade to the mean instead of aliasing.  The camera
 moves forward one unit per frame and yaws sinusoidally (bounded lateral drift).
+
+The KITTI-size (C2) sequence uses its own scene (``PRESET_SCENES``): half a unit per
+frame, seven texture octaves and no distance fading.  With the default scene the
+reference orchestration loses every landmark after a few hundred frames (its monocular
+scale collapses until the 1-unit minimum-depth gate rejects every triangulation,
+VisualOdometryPipeLine.py:149-168); with this one it tracks all 4541 frames from frame 0
+and from every 16-shard bootstrap (tools/scene_sweep.py).
 Rendering is plain torch in float64 using only elementwise IEEE operations (no BLAS,
 no library RNG), so a frame is bit-identical whether rendered on the CPU or the GPU
 and on any host; this module is data plumbing, not part of the VO hot path.
@@ -42,6 +49,10 @@ SIZES = {
     "malaga1024": (1024, 768),
     "hd1080": (1920, 1080),
 }
+
+
+def scene_for(preset: str) -> "SceneParams":
+    return PRESET_SCENES.get(preset, SceneParams())
 
 
 def intrinsics(name: str) -> np.ndarray:
@@ -80,6 +91,13 @@ class SceneParams:
     octaves: int = 10
     base_wavelength: float = 8.0  # world units of the coarsest octave
     persistence: float = 1.0
+    lod: bool = True              # fade octaves in with the pixel footprint (anti-aliasing)
+
+
+# scene per sequence preset (default SceneParams() otherwise); see the module docstring
+PRESET_SCENES = {
+    "kitti": SceneParams(speed=0.5, octaves=7, lod=False),
+}
 
 
 def poses(n_frames: int, p: SceneParams, start: int = 0):
@@ -135,7 +153,7 @@ class Renderer:
         self.W, self.H = SIZES[preset]
         self.K = intrinsics(preset)
         self.seed = int(seed)
-        self.p = params or SceneParams()
+        self.p = params or scene_for(preset)
         self.device = torch.device(device)
         fx, fy, cx, cy = (float(self.K[0, 0]), float(self.K[1, 1]), float(self.K[0, 2]),
                           float(self.K[1, 2]))
@@ -197,7 +215,7 @@ class Renderer:
         wl = p.base_wavelength
         norm = 0.0
         for o in range(p.octaves):
-            att = ((wl / foot - 2.0) / 2.0).clamp(0.0, 1.0)
+            att = ((wl / foot - 2.0) / 2.0).clamp(0.0, 1.0) if p.lod else 1.0
             sharp = (wl / foot / 1.5).clamp(1.0, 60.0)
             # per-surface lattice seed (seed*131 + surface*7919 + octave*31), one fused pass
             seed_t = which.to(torch.int64) * 7919 + (self.seed * 131 + o * 31)

@@ -26,8 +26,9 @@ sys.path.insert(0, REPO)
 CASES = [
     # name, sequence preset, seed, n_frames, snapshot frames
     ("parking_c1", "parking", 0, 100, (6, 30, 60, 99)),
-    ("kitti_c2", "kitti", 1, 40, (2, 20, 39)),
+    ("kitti_c2", "kitti", 1, 300, (2, 20, 39, 150, 299)),
     ("malaga_c3", "malaga", 2, 24, (6, 23)),
+    ("malaga1024_c3", "malaga1024", 2, 40, (6, 20, 39)),
 ]
 
 
@@ -90,7 +91,10 @@ def run_reference(preset, seed, n_frames, snaps):
 
 
 def main():
+    only = set(sys.argv[1:])
     for name, preset, seed, n, snaps in CASES:
+        if only and name not in only:
+            continue
         out, dt = run_reference(preset, seed, n, snaps)
         out["preset"] = np.asarray(preset)
         out["seed"] = np.asarray(seed)

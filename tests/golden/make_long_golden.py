@@ -1,0 +1,138 @@
+"""Long golden fixtures (run in the build container; ~30 min on 8 cores).
+
+The reference VisualOdometryPipeLine (/root/reference/VisualOdometryPipeLine.py, imported
+unchanged with the oracle shim as ``cv2``, as in make_golden.py) is run on the full
+KITTI-length synthetic C2 sequence (4541 frames, seed 1):
+
+  kitti_seq00.npz         one chain, bootstrap [0, 2], continuous_operation on 3..4540
+                          (main.py:112-124, :166-175): per frame t_CW, num_pts, N, P
+  kitti_seq00_shards.npz  the same sequence cut by shards.plan_shards into 8 (C4: one
+                          shard per GPU) and 16 shards (two per GPU / one GPU), each shard
+                          run by its own reference instance on its own boundaries (§8e)
+
+Frames are rendered once into a raw memmap (every frame's SHA-1 is stored, so the GPU
+tests can check their own renders), then the reference runs are spread over processes.
+Usage:  python tests/golden/make_long_golden.py [--procs 8]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+PRESET, SEED, N_FRAMES = "kitti", 1, 4541
+SHARD_COUNTS = (8, 16)
+OVERLAP = 30
+MEMMAP = "/tmp/vo_long_golden_frames.u8"
+
+
+def _render_chunk(args):
+    lo, hi, shape = args
+    import torch
+    torch.set_num_threads(1)
+    from monocular_visual_odometry_va4mr_amd.synth import Renderer
+    r = Renderer(PRESET, seed=SEED)
+    Rs, cs = r.gt_poses(N_FRAMES)
+    mm = np.memmap(MEMMAP, np.uint8, "r+", shape=shape)
+    for i in range(lo, hi, 4):
+        j = min(hi, i + 4)
+        mm[i:j] = r.render_batch(list(range(i, j)), Rs[i:j], cs[i:j]).numpy()
+    mm.flush()
+    return lo, hi
+
+
+def _run_ref(args):
+    """One reference instance over frames [start] + [boot1 .. end)."""
+    tag, start, boot1, end, shape = args
+    import oracle.cv2_oracle as cv2_oracle
+    sys.modules["cv2"] = cv2_oracle
+    sys.path.insert(0, "/root/reference")
+    import VisualOdometryPipeLine as ref  # the reference module, unmodified
+    from monocular_visual_odometry_va4mr_amd import options as O
+    from monocular_visual_odometry_va4mr_amd.synth import intrinsics
+    opts, _, _ = O.get(PRESET)
+    mm = np.memmap(MEMMAP, np.uint8, "r", shape=shape)
+    vo = ref.VisualOdometryPipeLine(intrinsics(PRESET), opts)
+    vo.initialization(np.array(mm[start]), np.array(mm[boot1]))
+    rows = [(vo.transforms[-1][1].ravel().copy(), int(vo.num_pts[-1]), len(vo.matched_landmarks),
+             int(vo.potential_keys.shape[0]))]
+    err = ""
+    t0 = time.time()
+    for i in range(boot1 + 1, end):
+        try:
+            vo.continuous_operation(np.array(mm[i]))
+        except Exception as e:  # the reference crashes here; record it
+            err = f"{type(e).__name__}: {e} (frame {i})"
+            break
+        rows.append((np.asarray(vo.transforms[-1][1], np.float64).ravel().copy(), int(vo.num_pts[-1]),
+                     len(vo.matched_landmarks), int(vo.potential_keys.shape[0])))
+    t = np.stack([r[0] for r in rows])
+    cnt = np.array([r[1:] for r in rows], np.int64)
+    print(f"  {tag} [{start},{end}): {len(rows)} poses in {time.time() - t0:.0f}s {err}", flush=True)
+    return tag, t, cnt, err
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--procs", type=int, default=8)
+    a = ap.parse_args()
+    from monocular_visual_odometry_va4mr_amd import options as O
+    from monocular_visual_odometry_va4mr_amd import shards as Sh
+    from monocular_visual_odometry_va4mr_amd.synth import SIZES
+    W, H = SIZES[PRESET]
+    shape = (N_FRAMES, H, W)
+    t0 = time.time()
+    if not os.path.exists(MEMMAP) or os.path.getsize(MEMMAP) != N_FRAMES * H * W:
+        np.memmap(MEMMAP, np.uint8, "w+", shape=shape).flush()
+        step = (N_FRAMES + 4 * a.procs - 1) // (4 * a.procs)
+        jobs = [(lo, min(N_FRAMES, lo + step), shape) for lo in range(0, N_FRAMES, step)]
+        with mp.get_context("fork").Pool(a.procs) as pool:
+            for lo, hi in pool.imap_unordered(_render_chunk, jobs):
+                pass
+        print(f"rendered {N_FRAMES} frames in {time.time() - t0:.0f}s", flush=True)
+    mm = np.memmap(MEMMAP, np.uint8, "r", shape=shape)
+    digests = np.stack([np.frombuffer(hashlib.sha1(np.ascontiguousarray(mm[i]).tobytes()).digest(), np.uint8)
+                        for i in range(N_FRAMES)])
+    _, (b0, b1), _ = O.get(PRESET)
+    gap = b1 - b0
+    jobs = [("full", 0, gap, N_FRAMES, shape)]
+    plans = {S: Sh.plan_shards(N_FRAMES, S, gap, OVERLAP) for S in SHARD_COUNTS}
+    for S, plan in plans.items():
+        jobs += [(f"s{S}_{s.index}", s.start, s.boot1, s.end, shape) for s in plan]
+    res = {}
+    with mp.get_context("fork").Pool(a.procs) as pool:
+        for tag, t, cnt, err in pool.imap_unordered(_run_ref, jobs):
+            res[tag] = (t, cnt, err)
+    full_t, full_cnt, full_err = res["full"]
+    np.savez_compressed(os.path.join(HERE, "kitti_seq00.npz"), preset=PRESET, seed=SEED, n_frames=N_FRAMES,
+                        boot=np.array([b0, b1]), t=full_t, num_pts=full_cnt[:, 0], N=full_cnt[:, 1],
+                        P=full_cnt[:, 2], error=np.asarray(full_err), digests=digests)
+    out = {"preset": PRESET, "seed": SEED, "n_frames": N_FRAMES, "overlap": OVERLAP}
+    for S, plan in plans.items():
+        ts, offs, errs, cnts = [], [0], [], []
+        for s in plan:
+            t, cnt, err = res[f"s{S}_{s.index}"]
+            ts.append(t)
+            cnts.append(cnt)
+            offs.append(offs[-1] + len(t))
+            errs.append(err)
+        out[f"s{S}_bounds"] = np.array([[s.start, s.boot1, s.end] for s in plan])
+        out[f"s{S}_t"] = np.concatenate(ts)
+        out[f"s{S}_counts"] = np.concatenate(cnts)
+        out[f"s{S}_off"] = np.array(offs)
+        out[f"s{S}_error"] = np.array(errs)
+    np.savez_compressed(os.path.join(HERE, "kitti_seq00_shards.npz"), **out)
+    print(f"done in {time.time() - t0:.0f}s; full chain: {len(full_t)} poses, error={full_err!r}")
+
+
+if __name__ == "__main__":
+    main()

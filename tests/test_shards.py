@@ -48,7 +48,9 @@ def test_stitch_recovers_global_trajectory():
         fr = np.array([s.start] + list(range(s.boot1, s.end)))
         # each shard sees its own frame: unknown scale / rotation / origin
         centres.append(_sim3(gt[fr], 0.5 + k, 0.2 * k, np.array([k, -k, 2.0 * k])))
-    out = Sh.stitch(sh, centres)
+    res = Sh.stitch(sh, centres)
+    assert res.breaks == [] and res.segments == [[0, 1, 2]]
+    out = res.positions
     # frames strictly between a shard's two bootstrap frames have no pose (as in the
     # reference, main.py:112-124); overlaps cover them for every shard but the first
     missing = np.nonzero(np.isnan(out[:, 0]))[0]
@@ -116,3 +118,125 @@ def test_gather_poses_gloo_world2():
     assert np.all(out[:2, :, :9] == 0) and np.all(out[2:, :, :9] == 1)
     assert np.all(out[:2, :, 9:12] == 10) and np.all(out[2:, :, 9:12] == 11)
     assert out[3, :, 12].tolist() == [1, 1, 1, 1, 0]
+
+
+def test_stitch_reports_coverage_break_instead_of_identity():
+    """A failed middle shard leaves its neighbours without common frames: the later shard
+    must open a new segment (reported as a break), not be placed at an identity Sim(3)."""
+    gt = _traj(300)
+    sh = Sh.plan_shards(300, 3, gap=2, overlap=30)
+    centres = []
+    for k, s in enumerate(sh):
+        fr = np.array([s.start] + list(range(s.boot1, s.end)))
+        centres.append(_sim3(gt[fr], 0.5 + k, 0.2 * k, np.array([k, -k, 2.0 * k])))
+    keep = [sh[0], sh[2]]                       # shard 1 failed and was dropped
+    res = Sh.stitch(keep, [centres[0], centres[2]])
+    assert res.breaks == [(0, 2, 0)]
+    assert res.segments == [[0], [2]]
+    s2 = sh[2]
+    f2 = np.array([s2.start] + list(range(s2.boot1, s2.end)))
+    assert (res.segment[f2] == 1).all()
+    # the second segment stays in its own frame (identical to shard 2's own centres) ...
+    assert np.allclose(res.positions[f2], centres[2])
+    # ... and the report evaluates each segment on its own, listing the break
+    from monocular_visual_odometry_va4mr_amd import evaluation as E
+    rep = E.shard_report(keep, [centres[0], centres[2]], gt, res)
+    st = rep["stitched"]
+    assert st["coverage_breaks"] == [[0, 2, 0]] and len(st["segments"]) == 2
+    assert all(seg["ate_rel"] < 1e-9 for seg in st["segments"])
+    assert "ate_rel" not in st
+
+
+class _StubRenderer:
+    """Frame source for run_sequence on CPU: a 'frame' is just its index."""
+
+    def __init__(self):
+        from monocular_visual_odometry_va4mr_amd.synth import SceneParams, intrinsics
+        self.p, self.K, self.W, self.H = SceneParams(), intrinsics("parking"), 4, 1
+
+    def render_batch(self, ids, R, c):
+        return torch.tensor([[float(i)] for i in ids], dtype=torch.float64)
+
+
+class _StubEngine:
+    """Stands in for engine.Engine: each chain appends the true camera centre of the frame it
+    is given, in its own Sim(3) frame; chain 1 of rank 0 fails at its 20th step, and every
+    chain 'fails' when fed the same frame twice (the padding after its shard has ended) --
+    which must not count against it."""
+
+    def __init__(self, K, opts, W, H, batch, device, ncap, pcap, fcap):
+        from types import SimpleNamespace
+        from monocular_visual_odometry_va4mr_amd.synth import SceneParams, poses
+        self.B = batch
+        self.dims = SimpleNamespace(fcap=fcap)
+        self.gt = poses(400, SceneParams())[1]
+        self.t = {"pose_R": torch.zeros(batch, fcap, 9, dtype=torch.float64),
+                  "pose_t": torch.zeros(batch, fcap, 3, dtype=torch.float64),
+                  "nF": torch.ones(batch, dtype=torch.int32), "status": torch.zeros(batch, dtype=torch.int32)}
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.last = [-1] * batch
+        self.steps = 0
+
+    def _append(self, b, f):
+        k = int(self.t["nF"][b])
+        sc = 0.5 + b + self.rank
+        self.t["pose_t"][b, k] = torch.from_numpy(sc * (self.gt[f] - self.gt[self.first[b]]))
+        self.t["pose_R"][b, k] = torch.eye(3, dtype=torch.float64).reshape(9)
+        self.t["nF"][b] = k + 1
+
+    def bootstrap(self, f0, f1):
+        self.first = [int(v) for v in f0[:, 0]]
+        for b in range(self.B):
+            self._append(b, int(f1[b, 0]))
+            self.last[b] = int(f1[b, 0])
+
+    def step(self, frames):
+        self.steps += 1
+        for b in range(self.B):
+            f = int(frames[b, 0])
+            if self.t["status"][b] != 0:
+                continue
+            if f == self.last[b] or (self.rank == 0 and b == 1 and self.steps == 20):
+                self.t["status"][b] = 1
+                continue
+            self._append(b, f)
+            self.last[b] = f
+
+
+def _seq_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"] = str(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from monocular_visual_odometry_va4mr_amd.run_sequence import run
+    res = run("parking", 200, 2, overlap=30, device="cpu", rank=rank, world=world,
+              engine_cls=_StubEngine, renderer=_StubRenderer())
+    q.put(None if res is None else {k: v for k, v in res.items() if not k.startswith("_")})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_sequence_bookkeeping_gloo_world2():
+    """run_sequence across 2 ranks (gloo): statuses are gathered with the poses, the failed
+    shard (rank 0, chain 1 = shard 1) is reported and dropped, the shard after it cannot be
+    chained and opens a new segment (coverage break), and chains that 'fail' only while
+    re-reading their last frame after their shard ended still count as complete."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seq_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rep = [r for r in res if r is not None][0]
+    assert rep["shards"] == 4 and rep["shards_ok"] == 3
+    assert [f["shard"] for f in rep["failed_shards"]] == [1]
+    st = rep["stitched"]
+    assert st["coverage_breaks"] == [[0, 2, 0]]
+    assert [s["shards"] for s in st["segments"]] == [[0], [2, 3]]
+    assert all(s["ate_rel"] < 1e-9 for s in st["segments"])
