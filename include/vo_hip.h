@@ -217,6 +217,14 @@ int vo_sift_plan(vo_sift_buf* sb, int W, int H);
 /* cv2.SIFT_create().detectAndCompute(img, None) (:35,226-227) for one image. */
 int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream);
 
+/* detectAndCompute for B images per launch sequence (the bootstrap of B chains, :226-227
+ * for every chain): image b at imgs + b * img_stride; every buffer of `sb` holds B
+ * consecutive per-image blocks of the size vo_sift_plan reports (gauss_floats, dog_floats,
+ * tmp_floats, 8 counters, cand_cap*4, kp_cap*{8,6,128,360}).  Image b's results are bit-
+ * identical to vo_sift on that image alone. */
+int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, int64_t img_stride, int W, int H,
+                  vo_stream_t stream);
+
 /* BFMatcher().knnMatch(q, t, k=2) (:36,229) for integer-valued float descriptors of
  * dim 128: bf16 MFMA distance tiles (exact), top-2 per query with OpenCV's tie order.
  * nq/nt are read on the device; idx2 [qcap][2] (-1 if absent), dist2 [qcap][2]. */

@@ -75,12 +75,32 @@ VO_DEV float fast_atan2(float y, float x)
     return a;
 }
 
+// ------------------------------------------------------- per-image views
+// vo_sift_batch runs B images per launch: every buffer of vo_sift_buf holds B consecutive
+// per-image blocks of the size vo_sift_plan reports; blockIdx.z is the image.
+VO_DEV vo_sift_buf sift_img(vo_sift_buf sb, int z)
+{
+    sb.gauss += (int64_t)z * sb.gauss_floats;
+    sb.dog += (int64_t)z * sb.dog_floats;
+    sb.tmp += (int64_t)z * sb.tmp_floats;
+    sb.counters += 8 * z;
+    sb.cand += (int64_t)z * sb.cand_cap * 4;
+    sb.kp += (int64_t)z * sb.kp_cap * 8;
+    sb.kp_out += (int64_t)z * sb.kp_cap * 6;
+    sb.desc += (int64_t)z * sb.kp_cap * 128;
+    sb.hist += (int64_t)z * sb.kp_cap * 360;
+    return sb;
+}
+
 // ------------------------------------------------------- scale space
-__global__ void k_upsample(const uint8_t* __restrict__ img, int w, int h, float* __restrict__ dst)
+__global__ void k_upsample(const uint8_t* __restrict__ img, int64_t img_stride, int w, int h, float* __restrict__ dst,
+                           int64_t dst_stride)
 {
     const int dx = blockIdx.x * blockDim.x + threadIdx.x, dy = blockIdx.y;
     const int dw = 2 * w;
     if (dx >= dw) return;
+    img += blockIdx.z * img_stride;
+    dst += blockIdx.z * dst_stride;
     float fy = (float)((dy + 0.5) * 0.5 - 0.5);
     int sy = (int)floorf(fy);
     fy -= sy;
@@ -100,33 +120,63 @@ __global__ void k_upsample(const uint8_t* __restrict__ img, int w, int h, float*
     dst[(int64_t)dy * dw + dx] = v0 * (1.f - fy) + v1 * fy;
 }
 
-__global__ void k_blur_h(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
-                         const float* __restrict__ kern, int n)
+// Separable Gaussian (BORDER_REFLECT_101) of one 64 x 32 output tile per block, both
+// passes through LDS: the source tile with its reflected halo is read from HBM once, the
+// row pass fills an LDS tile of (32 + 2r) rows, the column pass writes the output -- and,
+// when `dog` is given, the difference of Gaussians out - src at the same pixel (the next
+// DoG layer, D_i = G_{i+1} - G_i), so the DoG never re-reads the scale space.  Taps are
+// summed k = 0..n-1 in both passes, exactly as the two-pass form and the oracle do.
+#define BT_W 64
+#define BT_H 32
+#define BT_R 13                  // largest radius: ksize 27
+__global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src, int64_t src_stride,
+                                                   float* __restrict__ dst, int64_t dst_stride,
+                                                   float* __restrict__ dog, int64_t dog_stride, int w, int h,
+                                                   const float* __restrict__ kern, int n)
 {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= w) return;
-    const int r = n / 2;
-    const float* s = src + (int64_t)y * w;
-    float acc = 0.f;
-    for (int i = 0; i < n; ++i) acc += kern[i] * s[refl101(x - r + i, w)];
-    dst[(int64_t)y * w + x] = acc;
+    __shared__ float s_src[(BT_H + 2 * BT_R) * (BT_W + 2 * BT_R)];
+    __shared__ float s_row[(BT_H + 2 * BT_R) * BT_W];
+    __shared__ float s_k[2 * BT_R + 1];
+    const int tid = threadIdx.x;
+    const int r = n >> 1;
+    const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
+    src += blockIdx.z * src_stride;
+    dst += blockIdx.z * dst_stride;
+    if (tid < n) s_k[tid] = kern[tid];
+    const int rows = BT_H + 2 * r, cols = BT_W + 2 * r;
+    for (int i = tid; i < rows * cols; i += 256) {
+        const int ty = i / cols, tx = i - ty * cols;
+        const int gy = refl101(y0 - r + ty, h), gx = refl101(x0 - r + tx, w);
+        s_src[i] = src[(int64_t)gy * w + gx];
+    }
+    __syncthreads();
+    for (int i = tid; i < rows * BT_W; i += 256) {
+        const int ty = i >> 6, tx = i & (BT_W - 1);
+        const float* sp = s_src + ty * cols + tx;
+        float acc = 0.f;
+        for (int k = 0; k < n; ++k) acc += s_k[k] * sp[k];
+        s_row[i] = acc;
+    }
+    __syncthreads();
+    for (int i = tid; i < BT_H * BT_W; i += 256) {
+        const int ty = i >> 6, tx = i & (BT_W - 1);
+        const int gy = y0 + ty, gx = x0 + tx;
+        if (gy >= h || gx >= w) continue;
+        const float* sp = s_row + ty * BT_W + tx;
+        float acc = 0.f;
+        for (int k = 0; k < n; ++k) acc += s_k[k] * sp[k * BT_W];
+        dst[(int64_t)gy * w + gx] = acc;
+        if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc - s_src[(ty + r) * cols + tx + r];
+    }
 }
 
-__global__ void k_blur_v(const float* __restrict__ src, float* __restrict__ dst, int w, int h,
-                         const float* __restrict__ kern, int n)
-{
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-    if (x >= w) return;
-    const int r = n / 2;
-    float acc = 0.f;
-    for (int i = 0; i < n; ++i) acc += kern[i] * src[(int64_t)refl101(y - r + i, h) * w + x];
-    dst[(int64_t)y * w + x] = acc;
-}
-
-__global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh)
+__global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh,
+                          int64_t stride)
 {
     const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
     if (x >= dw) return;
+    src += blockIdx.z * stride;
+    dst += blockIdx.z * stride;
     const double ifx = 1. / ((double)dw / sw), ify = 1. / ((double)dh / sh);
     int sy = (int)floor(y * ify);
     if (sy > sh - 1) sy = sh - 1;
@@ -135,14 +185,9 @@ __global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* 
     dst[(int64_t)y * dw + x] = src[(int64_t)sy * sw + sx];
 }
 
-__global__ void k_dog(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ d, int64_t n)
+__global__ void k_extrema(vo_sift_buf sb_all, int o, int layer)
 {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) d[i] = b[i] - a[i];
-}
-
-__global__ void k_extrema(vo_sift_buf sb, int o, int layer)
-{
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     const int w = sb.oct_w[o], h = sb.oct_h[o];
     const int c = blockIdx.x * blockDim.x + threadIdx.x + SIFT_IMG_BORDER;
     const int r = blockIdx.y + SIFT_IMG_BORDER;
@@ -312,8 +357,9 @@ VO_DEV float orientation_hist(const float* img, int w, int h, int px, int py, in
     return maxval;
 }
 
-__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
+__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int nc = min(sb.counters[0], sb.cand_cap);
     if (k >= nc) return;
@@ -360,8 +406,9 @@ __global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
 //                 (k_sift_kp's temphist[36] is indexed dynamically, i.e. lives in scratch.)
 //                 Keypoints are appended with atomics; k_sift_sort_dedupe orders them.
 #define SIFT_REC 12
-__global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
+__global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     const int nc = min(sb.counters[0], sb.cand_cap);
     if (k >= nc) return;
@@ -378,118 +425,121 @@ __global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
     rec[7] = __int_as_float(r1); rec[8] = __int_as_float(c1);
 }
 
-__global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
+__global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     __shared__ int4 pb_s4[4][16];
     __shared__ float4 pv_s4[4][16];
     __shared__ float th_s[4][SIFT_ORI_HIST_BINS + 4];
     __shared__ float hs_s[4][SIFT_ORI_HIST_BINS];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + w;
     const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
-    if (q >= min(sb.counters[4], rec_cap)) return;
-    int* pbin = reinterpret_cast<int*>(pb_s4[w]);
-    float* pval = reinterpret_cast<float*>(pv_s4[w]);
-    const float* rec = sb.hist + (int64_t)SIFT_REC * q;
-    const float kx = rec[0], ky = rec[1], ksize = rec[2], kresp = rec[3];
-    const int koct = __float_as_int(rec[4]), o = __float_as_int(rec[5]), layer = __float_as_int(rec[6]);
-    const int py = __float_as_int(rec[7]), px = __float_as_int(rec[8]);
-    const float* tab = sb.consts + EXPTAB_OFF;
-    const float scl_octv = ksize * 0.5f / (float)(1 << o);
-    const float* img = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
-    const int wd = sb.oct_w[o], ht = sb.oct_h[o];
-    const int radius = __float2int_rn(SIFT_ORI_RADIUS * scl_octv);
-    const float sigma = SIFT_ORI_SIG_FCTR * scl_octv;
-    const int n = SIFT_ORI_HIST_BINS;
-    const float expf_scale = -1.f / (2.f * sigma * sigma);
-    const int side = 2 * radius + 1, total = side * side;
-    float th = 0.f;                                   // temphist[lane] for lane < 36
-    for (int base = 0; base < total; base += 64) {
-        const int pos = base + lane;
-        bool valid = false;
-        int bin = 0;
-        float val = 0.f;
-        if (pos < total) {
-            const int ii = pos / side;
-            const int i = ii - radius, j = pos - ii * side - radius;
-            const int y = py + i, x = px + j;
-            valid = y > 0 && y < ht - 1 && x > 0 && x < wd - 1;
+    const int n_rec = min(sb.counters[4], rec_cap);
+    for (int q = blockIdx.x * 4 + w; q < n_rec; q += gridDim.x * 4) {   // wave-uniform loop
+        int* pbin = reinterpret_cast<int*>(pb_s4[w]);
+        float* pval = reinterpret_cast<float*>(pv_s4[w]);
+        const float* rec = sb.hist + (int64_t)SIFT_REC * q;
+        const float kx = rec[0], ky = rec[1], ksize = rec[2], kresp = rec[3];
+        const int koct = __float_as_int(rec[4]), o = __float_as_int(rec[5]), layer = __float_as_int(rec[6]);
+        const int py = __float_as_int(rec[7]), px = __float_as_int(rec[8]);
+        const float* tab = sb.consts + EXPTAB_OFF;
+        const float scl_octv = ksize * 0.5f / (float)(1 << o);
+        const float* img = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
+        const int wd = sb.oct_w[o], ht = sb.oct_h[o];
+        const int radius = __float2int_rn(SIFT_ORI_RADIUS * scl_octv);
+        const float sigma = SIFT_ORI_SIG_FCTR * scl_octv;
+        const int n = SIFT_ORI_HIST_BINS;
+        const float expf_scale = -1.f / (2.f * sigma * sigma);
+        const int side = 2 * radius + 1, total = side * side;
+        float th = 0.f;                                   // temphist[lane] for lane < 36
+        for (int base = 0; base < total; base += 64) {
+            const int pos = base + lane;
+            bool valid = false;
+            int bin = 0;
+            float val = 0.f;
+            if (pos < total) {
+                const int ii = pos / side;
+                const int i = ii - radius, j = pos - ii * side - radius;
+                const int y = py + i, x = px + j;
+                valid = y > 0 && y < ht - 1 && x > 0 && x < wd - 1;
+                if (valid) {
+                    const float dx = DAT(img, wd, y, x + 1) - DAT(img, wd, y, x - 1);
+                    const float dy = DAT(img, wd, y - 1, x) - DAT(img, wd, y + 1, x);
+                    const float wt = exp32f((float)(i * i + j * j) * expf_scale, tab);
+                    const float ori = fast_atan2(dy, dx);
+                    const float mag = sqrtf(dx * dx + dy * dy);
+                    bin = __float2int_rn((n / 360.f) * ori);
+                    if (bin >= n) bin -= n;
+                    if (bin < 0) bin += n;
+                    val = wt * mag;
+                }
+            }
+            const uint64_t m = __ballot(valid);
+            const int nv = __popcll(m);
             if (valid) {
-                const float dx = DAT(img, wd, y, x + 1) - DAT(img, wd, y, x - 1);
-                const float dy = DAT(img, wd, y - 1, x) - DAT(img, wd, y + 1, x);
-                const float wt = exp32f((float)(i * i + j * j) * expf_scale, tab);
-                const float ori = fast_atan2(dy, dx);
-                const float mag = sqrtf(dx * dx + dy * dy);
-                bin = __float2int_rn((n / 360.f) * ori);
-                if (bin >= n) bin -= n;
-                if (bin < 0) bin += n;
-                val = wt * mag;
+                const int slot = __popcll(m & ((1ull << lane) - 1ull));
+                pbin[slot] = bin;
+                pval[slot] = val;
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // four pixels per step (entries past nv are masked to 0, which leaves th unchanged)
+            for (int p0 = 0; p0 < nv; p0 += 4) {
+                const int4 bb = *reinterpret_cast<const int4*>(pbin + p0);
+                const float4 vv = *reinterpret_cast<const float4*>(pval + p0);
+                th += (p0 + 0 < nv && bb.x == lane) ? vv.x : 0.f;
+                th += (p0 + 1 < nv && bb.y == lane) ? vv.y : 0.f;
+                th += (p0 + 2 < nv && bb.z == lane) ? vv.z : 0.f;
+                th += (p0 + 3 < nv && bb.w == lane) ? vv.w : 0.f;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        const uint64_t m = __ballot(valid);
-        const int nv = __popcll(m);
-        if (valid) {
-            const int slot = __popcll(m & ((1ull << lane) - 1ull));
-            pbin[slot] = bin;
-            pval[slot] = val;
-        }
+        float* t2 = th_s[w];                              // temphist[-2 .. n+1] at t2[0 .. n+3]
+        if (lane < n) t2[2 + lane] = th;
+        if (lane == n - 1) t2[1] = th;                    // temphist[-1] = temphist[n-1]
+        if (lane == n - 2) t2[0] = th;                    // temphist[-2] = temphist[n-2]
+        if (lane == 0) t2[n + 2] = th;                    // temphist[n] = temphist[0]
+        if (lane == 1) t2[n + 3] = th;                    // temphist[n+1] = temphist[1]
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // four pixels per step (entries past nv are masked to 0, which leaves th unchanged)
-        for (int p0 = 0; p0 < nv; p0 += 4) {
-            const int4 bb = *reinterpret_cast<const int4*>(pbin + p0);
-            const float4 vv = *reinterpret_cast<const float4*>(pval + p0);
-            th += (p0 + 0 < nv && bb.x == lane) ? vv.x : 0.f;
-            th += (p0 + 1 < nv && bb.y == lane) ? vv.y : 0.f;
-            th += (p0 + 2 < nv && bb.z == lane) ? vv.z : 0.f;
-            th += (p0 + 3 < nv && bb.w == lane) ? vv.w : 0.f;
+        float hv = -FLT_MAX;
+        if (lane < n) {
+            const float* t = t2 + 2 + lane;
+            hv = (t[-2] + t[2]) * (1.f / 16.f) + (t[-1] + t[1]) * (4.f / 16.f) + t[0] * (6.f / 16.f);
+            hs_s[w][lane] = hv;
         }
+        float omax = hv;
+    #pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off, 64));
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    float* t2 = th_s[w];                              // temphist[-2 .. n+1] at t2[0 .. n+3]
-    if (lane < n) t2[2 + lane] = th;
-    if (lane == n - 1) t2[1] = th;                    // temphist[-1] = temphist[n-1]
-    if (lane == n - 2) t2[0] = th;                    // temphist[-2] = temphist[n-2]
-    if (lane == 0) t2[n + 2] = th;                    // temphist[n] = temphist[0]
-    if (lane == 1) t2[n + 3] = th;                    // temphist[n+1] = temphist[1]
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float hv = -FLT_MAX;
-    if (lane < n) {
-        const float* t = t2 + 2 + lane;
-        hv = (t[-2] + t[2]) * (1.f / 16.f) + (t[-1] + t[1]) * (4.f / 16.f) + t[0] * (6.f / 16.f);
-        hs_s[w][lane] = hv;
-    }
-    float omax = hv;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) omax = fmaxf(omax, __shfl_xor(omax, off, 64));
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
-    if (lane < n) {
-        const float* hist = hs_s[w];
-        const int j = lane;
-        const int l = j > 0 ? j - 1 : n - 1;
-        const int r2 = j < n - 1 ? j + 1 : 0;
-        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
-            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
-            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
-            float angle = 360.f - (float)((360.f / n) * bin);
-            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-            const int qo = atomicAdd(&sb.counters[1], 1);
-            if (qo < sb.kp_cap) {
-                float* out = sb.kp + 8 * (int64_t)qo;
-                out[0] = kx; out[1] = ky; out[2] = ksize; out[3] = angle; out[4] = kresp;
-                out[5] = __int_as_float(koct); out[6] = 0.f; out[7] = 0.f;
-            } else {
-                sb.counters[3] = 1;
+        const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
+        if (lane < n) {
+            const float* hist = hs_s[w];
+            const int j = lane;
+            const int l = j > 0 ? j - 1 : n - 1;
+            const int r2 = j < n - 1 ? j + 1 : 0;
+            if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+                float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
+                bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+                float angle = 360.f - (float)((360.f / n) * bin);
+                if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+                const int qo = atomicAdd(&sb.counters[1], 1);
+                if (qo < sb.kp_cap) {
+                    float* out = sb.kp + 8 * (int64_t)qo;
+                    out[0] = kx; out[1] = ky; out[2] = ksize; out[3] = angle; out[4] = kresp;
+                    out[5] = __int_as_float(koct); out[6] = 0.f; out[7] = 0.f;
+                } else {
+                    sb.counters[3] = 1;
+                }
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -507,8 +557,9 @@ VO_DEV bool kp_less(const float* a, const float* b)
 }
 
 #define SORT_N 16384
-__global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
+__global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     __shared__ int idx[SORT_N];
     __shared__ int lds[16];
     const int tid = threadIdx.x;
@@ -563,8 +614,9 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
     if (tid == 0) sb.counters[2] = out;
 }
 
-__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
+__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= sb.counters[2]) return;
     const float* tab = sb.consts + EXPTAB_OFF;
@@ -671,8 +723,9 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
 //  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
 #define SIFT_HITMASK ((1ull << 0) | (1ull << 1) | (1ull << 6) | (1ull << 7) | (1ull << 10) | (1ull << 11) | \
                       (1ull << 60) | (1ull << 61))
-__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
+__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb_all)
 {
+    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
     int (*pidx_s)[64] = reinterpret_cast<int (*)[64]>(pidx_s4);
     __shared__ float pval_s[4][64 * 8];
@@ -680,165 +733,167 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
     __shared__ float dst_s[4][128];
     __shared__ float red_s[4][2];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + w;
-    if (q >= sb.counters[2]) return;
-    int* pidx = pidx_s[w];
-    float* pval = pval_s[w];
-    float* hist = hist_s[w];
-    float* dsl = dst_s[w];
-    const float* tab = sb.consts + EXPTAB_OFF;
-    const float* kp = sb.kp_out + 6 * (int64_t)q;
-    const int kpo = (int)kp[5];
-    int octave = kpo & 255, layer = (kpo >> 8) & 255;
-    octave = octave < 128 ? octave : (-128 | octave);
-    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
-    const float size = kp[2] * scale;
-    const float ptx = kp[0] * scale, pty = kp[1] * scale;
-    const int oi = octave + 1;
-    const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
-    const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
-    float angle = 360.f - kp[3];
-    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-    const float ori = angle, scl = size * 0.5f;
-    const int d = 4, n = 8;
-    const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
-    float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
-    float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
-    const float bins_per_rad = n / 360.f;
-    const float exp_scale = -1.f / (d * d * 0.5f);
-    const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
-    int radius = __float2int_rn(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
-    const int rmax = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
-    if (radius > rmax) radius = rmax;
-    cos_t /= hist_width;
-    sin_t /= hist_width;
-    const int side = 2 * radius + 1;
-    const int total = side * side;
-    float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, h4 = 0.f, h5 = 0.f;
-    for (int base = 0; base < total; base += 64) {
-        const int pos = base + lane;
-        bool valid = false;
-        int idx = 0;
-        float vv[8];
-        if (pos < total) {
-            const int ii = pos / side;
-            const int i = ii - radius, j = pos - ii * side - radius;
-            const float c_rot = j * cos_t - i * sin_t;
-            const float r_rot = j * sin_t + i * cos_t;
-            float rbin = r_rot + d / 2 - 0.5f;
-            float cbin = c_rot + d / 2 - 0.5f;
-            const int r = ptiy + i, c = ptix + j;
-            valid = rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+    const int n_kp = sb.counters[2];
+    for (int q = blockIdx.x * 4 + w; q < n_kp; q += gridDim.x * 4) {     // wave-uniform loop
+        int* pidx = pidx_s[w];
+        float* pval = pval_s[w];
+        float* hist = hist_s[w];
+        float* dsl = dst_s[w];
+        const float* tab = sb.consts + EXPTAB_OFF;
+        const float* kp = sb.kp_out + 6 * (int64_t)q;
+        const int kpo = (int)kp[5];
+        int octave = kpo & 255, layer = (kpo >> 8) & 255;
+        octave = octave < 128 ? octave : (-128 | octave);
+        const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
+        const float size = kp[2] * scale;
+        const float ptx = kp[0] * scale, pty = kp[1] * scale;
+        const int oi = octave + 1;
+        const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
+        const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
+        float angle = 360.f - kp[3];
+        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        const float ori = angle, scl = size * 0.5f;
+        const int d = 4, n = 8;
+        const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
+        float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
+        float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
+        const float bins_per_rad = n / 360.f;
+        const float exp_scale = -1.f / (d * d * 0.5f);
+        const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
+        int radius = __float2int_rn(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+        const int rmax = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
+        if (radius > rmax) radius = rmax;
+        cos_t /= hist_width;
+        sin_t /= hist_width;
+        const int side = 2 * radius + 1;
+        const int total = side * side;
+        float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, h4 = 0.f, h5 = 0.f;
+        for (int base = 0; base < total; base += 64) {
+            const int pos = base + lane;
+            bool valid = false;
+            int idx = 0;
+            float vv[8];
+            if (pos < total) {
+                const int ii = pos / side;
+                const int i = ii - radius, j = pos - ii * side - radius;
+                const float c_rot = j * cos_t - i * sin_t;
+                const float r_rot = j * sin_t + i * cos_t;
+                float rbin = r_rot + d / 2 - 0.5f;
+                float cbin = c_rot + d / 2 - 0.5f;
+                const int r = ptiy + i, c = ptix + j;
+                valid = rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
+                if (valid) {
+                    const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
+                    const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
+                    const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
+                    const float o = fast_atan2(dy, dx);
+                    const float mag = sqrtf(dx * dx + dy * dy) * wgt;
+                    float obin = (o - ori) * bins_per_rad;
+                    int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
+                    rbin -= r0; cbin -= c0; obin -= o0;
+                    if (o0 < 0) o0 += n;
+                    if (o0 >= n) o0 -= n;
+                    const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                    const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                    const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                    const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                    const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                    const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                    const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                    idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+                    // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
+                    vv[0] = v_rco000; vv[1] = v_rco001; vv[2] = v_rco010; vv[3] = v_rco011;
+                    vv[4] = v_rco100; vv[5] = v_rco101; vv[6] = v_rco110; vv[7] = v_rco111;
+                }
+            }
+            const uint64_t m = __ballot(valid);
+            const int nv = __popcll(m);
             if (valid) {
-                const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
-                const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
-                const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
-                const float o = fast_atan2(dy, dx);
-                const float mag = sqrtf(dx * dx + dy * dy) * wgt;
-                float obin = (o - ori) * bins_per_rad;
-                int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
-                rbin -= r0; cbin -= c0; obin -= o0;
-                if (o0 < 0) o0 += n;
-                if (o0 >= n) o0 -= n;
-                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-                // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
-                vv[0] = v_rco000; vv[1] = v_rco001; vv[2] = v_rco010; vv[3] = v_rco011;
-                vv[4] = v_rco100; vv[5] = v_rco101; vv[6] = v_rco110; vv[7] = v_rco111;
+                const int slot = __popcll(m & ((1ull << lane) - 1ull));
+                pidx[slot] = idx;
+    #pragma unroll
+                for (int k = 0; k < 8; ++k) pval[slot * 8 + k] = vv[k];
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // four pixels per step: their LDS reads are issued together, the additions stay in
+            // pixel order (pidx is padded to a multiple of 4 with a bin no lane owns... see below)
+            for (int p0 = 0; p0 < nv; p0 += 4) {
+                const int4 ids = *reinterpret_cast<const int4*>(pidx + p0);
+                const int idv[4] = {ids.x, ids.y, ids.z, ids.w};
+                float vv4[4];
+                int kk4[4];
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int id = idv[u];
+                    const int off = (lane - id) & 63;
+                    const bool hit = p0 + u < nv && ((SIFT_HITMASK >> off) & 1ull);
+                    // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
+                    const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
+                    vv4[u] = hit ? pval[(p0 + u) * 8 + sl] : 0.f;
+                    const int real = off + (off == 6 || off == 7 ? 64 : 0);
+                    kk4[u] = (id + real - lane) >> 6;
+                }
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float v = vv4[u];
+                    const int k = kk4[u];
+                    h0 += k == 0 ? v : 0.f;
+                    h1 += k == 1 ? v : 0.f;
+                    h2 += k == 2 ? v : 0.f;
+                    h3 += k == 3 ? v : 0.f;
+                    h4 += k == 4 ? v : 0.f;
+                    h5 += k == 5 ? v : 0.f;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        const uint64_t m = __ballot(valid);
-        const int nv = __popcll(m);
-        if (valid) {
-            const int slot = __popcll(m & ((1ull << lane) - 1ull));
-            pidx[slot] = idx;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pval[slot * 8 + k] = vv[k];
+        hist[lane] = h0; hist[lane + 64] = h1; hist[lane + 128] = h2;
+        hist[lane + 192] = h3; hist[lane + 256] = h4; hist[lane + 320] = h5;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // circular orientation wrap + copy (independent per output)
+        for (int t = lane; t < d * d * n; t += 64) {
+            const int cell = t / n, k = t - cell * n;
+            const int i = cell / d, j = cell - i * d;
+            const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+            float v = hist[idx + k];
+            if (k < 2) v += hist[idx + n + k];
+            dsl[t] = v;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // four pixels per step: their LDS reads are issued together, the additions stay in
-        // pixel order (pidx is padded to a multiple of 4 with a bin no lane owns... see below)
-        for (int p0 = 0; p0 < nv; p0 += 4) {
-            const int4 ids = *reinterpret_cast<const int4*>(pidx + p0);
-            const int idv[4] = {ids.x, ids.y, ids.z, ids.w};
-            float vv4[4];
-            int kk4[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int id = idv[u];
-                const int off = (lane - id) & 63;
-                const bool hit = p0 + u < nv && ((SIFT_HITMASK >> off) & 1ull);
-                // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
-                const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
-                vv4[u] = hit ? pval[(p0 + u) * 8 + sl] : 0.f;
-                const int real = off + (off == 6 || off == 7 ? 64 : 0);
-                kk4[u] = (id + real - lane) >> 6;
+        const int len = d * d * n;
+        if (lane == 0) {
+            float nrm2 = 0;
+            for (int k = 0; k < len; ++k) nrm2 += dsl[k] * dsl[k];
+            const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
+            nrm2 = 0;
+            for (int i = 0; i < len; ++i) {
+                const float v = dsl[i] < thr ? dsl[i] : thr;
+                nrm2 += v * v;
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const float v = vv4[u];
-                const int k = kk4[u];
-                h0 += k == 0 ? v : 0.f;
-                h1 += k == 1 ? v : 0.f;
-                h2 += k == 2 ? v : 0.f;
-                h3 += k == 3 ? v : 0.f;
-                h4 += k == 4 ? v : 0.f;
-                h5 += k == 5 ? v : 0.f;
-            }
+            red_s[w][0] = thr;
+            red_s[w][1] = nrm2;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    hist[lane] = h0; hist[lane + 64] = h1; hist[lane + 128] = h2;
-    hist[lane + 192] = h3; hist[lane + 256] = h4; hist[lane + 320] = h5;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // circular orientation wrap + copy (independent per output)
-    for (int t = lane; t < d * d * n; t += 64) {
-        const int cell = t / n, k = t - cell * n;
-        const int i = cell / d, j = cell - i * d;
-        const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
-        float v = hist[idx + k];
-        if (k < 2) v += hist[idx + n + k];
-        dsl[t] = v;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int len = d * d * n;
-    if (lane == 0) {
-        float nrm2 = 0;
-        for (int k = 0; k < len; ++k) nrm2 += dsl[k] * dsl[k];
-        const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
-        nrm2 = 0;
-        for (int i = 0; i < len; ++i) {
-            const float v = dsl[i] < thr ? dsl[i] : thr;
-            nrm2 += v * v;
+        const float thr = red_s[w][0];
+        const float s2 = sqrtf(red_s[w][1]);
+        const float nscale = SIFT_INT_DESCR_FCTR / (s2 > FLT_EPSILON ? s2 : FLT_EPSILON);
+        float* dst = sb.desc + 128 * (int64_t)q;
+        for (int t = lane; t < len; t += 64) {
+            const float v = dsl[t] < thr ? dsl[t] : thr;
+            const int iv = __float2int_rn(v * nscale);
+            dst[t] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
         }
-        red_s[w][0] = thr;
-        red_s[w][1] = nrm2;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float thr = red_s[w][0];
-    const float s2 = sqrtf(red_s[w][1]);
-    const float nscale = SIFT_INT_DESCR_FCTR / (s2 > FLT_EPSILON ? s2 : FLT_EPSILON);
-    float* dst = sb.desc + 128 * (int64_t)q;
-    for (int t = lane; t < len; t += 64) {
-        const float v = dsl[t] < thr ? dsl[t] : thr;
-        const int iv = __float2int_rn(v * nscale);
-        dst[t] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -999,17 +1054,15 @@ static void gauss_kernel(int n, double sigma, float* k)
     for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
 }
 
-static void blur(const vo_sift_buf* sb, const float* src, float* dst, int w, int h, const float* kern_dev, int n,
-                 hipStream_t st)
-{
-    dim3 g((w + 127) / 128, h);
-    hipLaunchKernelGGL(k_blur_h, g, dim3(128), 0, st, src, sb->tmp, w, h, kern_dev, n);
-    hipLaunchKernelGGL(k_blur_v, g, dim3(128), 0, st, (const float*)sb->tmp, dst, w, h, kern_dev, n);
-}
+// blocks per image of the wave-per-keypoint kernels (they loop over their items)
+#define SIFT_WAVE_BLOCKS 512
 
-extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream)
+extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, int64_t img_stride, int W, int H,
+                             vo_stream_t stream)
 {
-    if (!sb || !img || sb->W != W || sb->H != H || !sb->gauss || !sb->dog || !sb->tmp || !sb->consts) return VO_EARG;
+    if (!sb || !imgs || B < 1 || B > 65535 || sb->W != W || sb->H != H || !sb->gauss || !sb->dog || !sb->tmp ||
+        !sb->consts || img_stride < (int64_t)W * H)
+        return VO_EARG;
     hipStream_t st = VO_STREAM(stream);
     // host-side constants with the C library's exp/pow (as the oracle): kernel 0 = base blur,
     // kernels 1..5 = layer increments, then the exp32f table.  They depend on nothing but the
@@ -1048,56 +1101,59 @@ extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, 
     const int* ks = SC.ks;
     if (hipMemcpyAsync(sb->consts, SC.host, sizeof(float) * (EXPTAB_OFF + 64), hipMemcpyHostToDevice, st) != hipSuccess)
         return VO_EHIP;
-    if (hipMemsetAsync(sb->counters, 0, 8 * sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
-    // base: 2x upsample + blur to sigma
-    float* g0 = sb->gauss + sb->gauss_off[0];
-    hipLaunchKernelGGL(k_upsample, dim3((2 * W + 127) / 128, 2 * H), dim3(128), 0, st, img, W, H, g0);
-    blur(sb, g0, g0, 2 * W, 2 * H, sb->consts, ks[0], st);
-    for (int o = 0; o < sb->n_oct; ++o)
-        for (int i = 0; i < N_LAYERS + 3; ++i) {
-            if (o == 0 && i == 0) continue;
-            float* dst = sb->gauss + sb->gauss_off[o * 6 + i];
-            const int w = sb->oct_w[o], h = sb->oct_h[o];
-            if (w < 1 || h < 1) continue;
-            if (i == 0) {
-                const float* src = sb->gauss + sb->gauss_off[(o - 1) * 6 + N_LAYERS];
-                hipLaunchKernelGGL(k_nn_down, dim3((w + 127) / 128, h), dim3(128), 0, st, src, sb->oct_w[o - 1],
-                                   sb->oct_h[o - 1], dst, w, h);
-            } else {
-                blur(sb, sb->gauss + sb->gauss_off[o * 6 + i - 1], dst, w, h, sb->consts + i * KTAPS, ks[i], st);
-            }
+    if (hipMemsetAsync(sb->counters, 0, 8 * sizeof(int32_t) * (size_t)B, st) != hipSuccess) return VO_EHIP;
+    const unsigned nb = (unsigned)B;
+    const int64_t gs = sb->gauss_floats, ds = sb->dog_floats;
+    // base: 2x upsample (into the blur scratch) + blur to sigma
+    hipLaunchKernelGGL(k_upsample, dim3((2 * W + 127) / 128, 2 * H, nb), dim3(128), 0, st, imgs, img_stride, W, H,
+                       sb->tmp, sb->tmp_floats);
+    auto blur = [&](const float* src, int64_t src_stride, float* dst, float* dog, int w, int h, int layer) {
+        dim3 g((w + BT_W - 1) / BT_W, (h + BT_H - 1) / BT_H, nb);
+        hipLaunchKernelGGL(k_blur_tile, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h,
+                           (const float*)(sb->consts + layer * KTAPS), ks[layer]);
+    };
+    blur(sb->tmp, sb->tmp_floats, sb->gauss + sb->gauss_off[0], nullptr, 2 * W, 2 * H, 0);
+    for (int o = 0; o < sb->n_oct; ++o) {
+        const int w = sb->oct_w[o], h = sb->oct_h[o];
+        if (w < 1 || h < 1) continue;
+        if (o > 0) {
+            const float* src = sb->gauss + sb->gauss_off[(o - 1) * 6 + N_LAYERS];
+            hipLaunchKernelGGL(k_nn_down, dim3((w + 127) / 128, h, nb), dim3(128), 0, st, src, sb->oct_w[o - 1],
+                               sb->oct_h[o - 1], sb->gauss + sb->gauss_off[o * 6], w, h, gs);
         }
-    for (int o = 0; o < sb->n_oct; ++o)
-        for (int i = 0; i < N_LAYERS + 2; ++i) {
-            const int64_t n = (int64_t)sb->oct_w[o] * sb->oct_h[o];
-            if (n <= 0) continue;
-            hipLaunchKernelGGL(k_dog, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                               (const float*)(sb->gauss + sb->gauss_off[o * 6 + i]),
-                               (const float*)(sb->gauss + sb->gauss_off[o * 6 + i + 1]), sb->dog + sb->dog_off[o * 5 + i], n);
-        }
+        // G_i = blur(G_{i-1}); the same pass writes D_{i-1} = G_i - G_{i-1}
+        for (int i = 1; i < N_LAYERS + 3; ++i)
+            blur(sb->gauss + sb->gauss_off[o * 6 + i - 1], gs, sb->gauss + sb->gauss_off[o * 6 + i],
+                 sb->dog + sb->dog_off[o * 5 + i - 1], w, h, i);
+    }
     for (int o = 0; o < sb->n_oct; ++o) {
         const int w = sb->oct_w[o], h = sb->oct_h[o];
         if (w <= 2 * SIFT_IMG_BORDER || h <= 2 * SIFT_IMG_BORDER) continue;
         for (int i = 1; i <= N_LAYERS; ++i)
-            hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER), dim3(128), 0,
-                               st, *sb, o, i);
+            hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER, nb),
+                               dim3(128), 0, st, *sb, o, i);
     }
     const char* kser = getenv("VO_SIFT_KP_SERIAL");
     if (kser && atoi(kser) == 1) {
-        hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128, 1, nb), dim3(128), 0, st, *sb);
     } else {
-        hipLaunchKernelGGL(k_sift_refine, dim3((sb->cand_cap + 127) / 128), dim3(128), 0, st, *sb);
-        hipLaunchKernelGGL(k_sift_ori, dim3((sb->cand_cap + 3) / 4), dim3(256), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_refine, dim3((sb->cand_cap + 127) / 128, 1, nb), dim3(128), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_ori, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
     }
-    hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1), dim3(1024), 0, st, *sb);
+    hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1, 1, nb), dim3(1024), 0, st, *sb);
     // wave-per-keypoint descriptor kernel unless VO_SIFT_DESC_SERIAL=1 (thread per keypoint;
     // both produce identical descriptors)
     const char* ser = getenv("VO_SIFT_DESC_SERIAL");
     if (ser && atoi(ser) == 1)
-        hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64), dim3(64), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64, 1, nb), dim3(64), 0, st, *sb);
     else
-        hipLaunchKernelGGL(k_sift_desc_w, dim3((sb->kp_cap + 3) / 4), dim3(256), 0, st, *sb);
+        hipLaunchKernelGGL(k_sift_desc_w, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
     return hip_rc();
+}
+
+extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream)
+{
+    return vo_sift_batch(sb, 1, img, (int64_t)W * H, W, H, stream);
 }
 
 extern "C" int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt, int32_t qcap,

@@ -303,59 +303,61 @@ class Engine:
         self.replay_step()
 
     # ------------------------------------------------------------------ bootstrap
-    def bootstrap(self, img0, img1):
+    def bootstrap(self, img0, img1, sift_batch_bytes: int | None = None):
         """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:
         SIFT on both frames, BF 2-NN + ratio test, 5-point E-RANSAC, inlier split,
         recoverPose, t *= sign(t_z), triangulation, pose append; then potential_frame
-        = img1 (its pyramid + derivatives become pyr[prev])."""
-        from .features import Sift, bf_knn2
+        = img1 (its pyramid + derivatives become pyr[prev]).
+
+        Batched across chains: the chains are taken in chunks whose SIFT scale spaces fit
+        ``sift_batch_bytes`` (default 12 GB, env VO_SIFT_BATCH_BYTES); per chunk one
+        vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
+        and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync until
+        the capacity check at the end."""
+        from .features import Sift, bf_knn2_batch
         img0 = self._frames(img0)
         img1 = self._frames(img1)
         d = self.dims
         dev = self.device
-        if getattr(self, "_sift", None) is None:
-            self._sift = Sift(self.W, self.H, dev)
+        B = self.B
+        budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 12 << 30))
+        per_img = Sift.bytes_per_image(self.W, self.H)
+        m = max(1, min(B, budget // (2 * per_img)))          # chains per chunk
+        if getattr(self, "_sift", None) is None or self._sift.batch < 2 * m:
+            self._sift = None
+            torch.cuda.empty_cache()
+            self._sift = Sift(self.W, self.H, dev, batch=2 * m)
         sift = self._sift
         kcap = sift.kp_cap
-        B = self.B
-        kp0 = torch.zeros((B, kcap, 6), dtype=torch.float32, device=dev)
-        kp1 = torch.zeros_like(kp0)
-        n0 = torch.zeros(B, dtype=torch.int32, device=dev)
-        n1 = torch.zeros_like(n0)
-        idx2 = torch.full((B, kcap, 2), -1, dtype=torch.int32, device=dev)
-        dist2 = torch.zeros((B, kcap, 2), dtype=torch.float32, device=dev)
-        desc0 = torch.zeros((kcap, 128), dtype=torch.float32, device=dev)
-        for b in range(B):
-            k, dsc, n = sift.run(img0[b])
-            kp0[b].copy_(k)
-            desc0.copy_(dsc)
-            n0[b:b + 1].copy_(n)
-            overflow0 = sift.t["counters"][3].clone()
-            k, dsc, n = sift.run(img1[b])
-            kp1[b].copy_(k)
-            n1[b:b + 1].copy_(n)
-            i2, d2 = bf_knn2(desc0, n0[b:b + 1], dsc, n, kcap)
-            idx2[b].copy_(i2)
-            dist2[b].copy_(d2)
-            if int(overflow0) or sift.overflowed():
-                raise RuntimeError("SIFT capacity exceeded")
         cap = min(d.ncap, d.pcap, kcap)
         pts0 = torch.zeros((B, cap, 2), dtype=torch.float32, device=dev)
         pts1 = torch.zeros_like(pts0)
         cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        n0 = torch.zeros(B, dtype=torch.int32, device=dev)
+        n1 = torch.zeros_like(n0)
+        overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         st = self.stream
-        self._chk(self.lib.vo_ratio_matches(B, C.c_void_p(kp0.data_ptr()), C.c_void_p(kp1.data_ptr()), kcap,
-                                            C.c_void_p(idx2.data_ptr()), C.c_void_p(dist2.data_ptr()),
-                                            C.c_void_p(n0.data_ptr()), kcap, float(self.opts.feature_ratio),
-                                            C.c_void_p(pts0.data_ptr()), C.c_void_p(pts1.data_ptr()),
-                                            C.c_void_p(cnt.data_ptr()), cap, st), "vo_ratio_matches")
+        for c0 in range(0, B, m):
+            c1 = min(B, c0 + m)
+            k = c1 - c0
+            kp, desc, n = sift.run_batch(torch.cat([img0[c0:c1], img1[c0:c1]]))
+            overflow = torch.maximum(overflow, sift.t["counters"][:2 * k, 3].max().reshape(1))
+            n0[c0:c1] = n[:k]
+            n1[c0:c1] = n[k:]
+            idx2, dist2 = bf_knn2_batch(desc[:k], n[:k], desc[k:], n[k:])
+            self._chk(self.lib.vo_ratio_matches(k, C.c_void_p(kp[:k].data_ptr()), C.c_void_p(kp[k:].data_ptr()), kcap,
+                                                C.c_void_p(idx2.data_ptr()), C.c_void_p(dist2.data_ptr()),
+                                                C.c_void_p(n[:k].data_ptr()), kcap, float(self.opts.feature_ratio),
+                                                C.c_void_p(pts0[c0:c1].data_ptr()), C.c_void_p(pts1[c0:c1].data_ptr()),
+                                                C.c_void_p(cnt[c0:c1].data_ptr()), cap, st), "vo_ratio_matches")
         self._chk(self.lib.vo_bootstrap(self._pd, self._po, self._ps, C.c_void_p(pts0.data_ptr()),
                                         C.c_void_p(pts1.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, st),
                   "vo_bootstrap")
         self.prev = 0
         self.build_pyramid(img1, self.prev)
-        self._boot_debug = {"kp0": kp0, "kp1": kp1, "n0": n0, "n1": n1, "idx2": idx2, "dist2": dist2,
-                            "pts0": pts0, "pts1": pts1, "cnt": cnt}
+        if int(overflow):
+            raise RuntimeError("SIFT capacity exceeded")
+        self._boot_debug = {"n0": n0, "n1": n1, "pts0": pts0, "pts1": pts1, "cnt": cnt}
 
     # ------------------------------------------------------------------ state I/O
     def import_chain(self, b: int, *, landmarks, keypoints, cand, cand_first, cand_tau, transforms,

@@ -12,26 +12,31 @@ from . import _lib as L
 
 
 class Sift:
-    """SIFT for one image size on one device (OpenCV 4.6 defaults)."""
+    """SIFT for one image size on one device (OpenCV 4.6 defaults), ``batch`` images per
+    launch sequence (vo_sift_batch).  Buffers hold ``batch`` per-image blocks: results of
+    image b are kp_out[b], desc[b], counters[b, 2]."""
 
-    def __init__(self, width: int, height: int, device=None, cand_cap: int = 131072, kp_cap: int = 16384):
+    def __init__(self, width: int, height: int, device=None, cand_cap: int = 131072, kp_cap: int = 16384,
+                 batch: int = 1):
         self.lib = L.lib()
         self.device = torch.device(device or "cuda")
         self.W, self.H = int(width), int(height)
+        self.batch = int(batch)
         sb = L.VoSiftBuf()
         L.check(self.lib.vo_sift_plan(C.byref(sb), self.W, self.H), "vo_sift_plan")
         dev = self.device
+        n = self.batch
         self.t = {
-            "gauss": torch.empty(sb.gauss_floats, dtype=torch.float32, device=dev),
-            "dog": torch.empty(sb.dog_floats, dtype=torch.float32, device=dev),
-            "tmp": torch.empty(sb.tmp_floats, dtype=torch.float32, device=dev),
+            "gauss": torch.empty(n * sb.gauss_floats, dtype=torch.float32, device=dev),
+            "dog": torch.empty(n * sb.dog_floats, dtype=torch.float32, device=dev),
+            "tmp": torch.empty(n * sb.tmp_floats, dtype=torch.float32, device=dev),
             "consts": torch.zeros(7 * 32 + 64, dtype=torch.float32, device=dev),
-            "counters": torch.zeros(8, dtype=torch.int32, device=dev),
-            "cand": torch.empty(cand_cap * 4, dtype=torch.int32, device=dev),
-            "kp": torch.empty(kp_cap * 8, dtype=torch.float32, device=dev),
-            "kp_out": torch.zeros(kp_cap, 6, dtype=torch.float32, device=dev),
-            "desc": torch.zeros(kp_cap, 128, dtype=torch.float32, device=dev),
-            "hist": torch.empty(kp_cap * 360, dtype=torch.float32, device=dev),
+            "counters": torch.zeros(n, 8, dtype=torch.int32, device=dev),
+            "cand": torch.empty(n * cand_cap * 4, dtype=torch.int32, device=dev),
+            "kp": torch.empty(n * kp_cap * 8, dtype=torch.float32, device=dev),
+            "kp_out": torch.zeros(n, kp_cap, 6, dtype=torch.float32, device=dev),
+            "desc": torch.zeros(n, kp_cap, 128, dtype=torch.float32, device=dev),
+            "hist": torch.empty(n * kp_cap * 360, dtype=torch.float32, device=dev),
         }
         for k, v in self.t.items():
             setattr(sb, k, v.data_ptr())
@@ -39,24 +44,44 @@ class Sift:
         self.sb = sb
         self.kp_cap = int(kp_cap)
 
+    @staticmethod
+    def bytes_per_image(width: int, height: int, cand_cap: int = 131072, kp_cap: int = 16384) -> int:
+        sb = L.VoSiftBuf()
+        L.check(L.lib().vo_sift_plan(C.byref(sb), int(width), int(height)), "vo_sift_plan")
+        return 4 * (sb.gauss_floats + sb.dog_floats + sb.tmp_floats + 8 + cand_cap * 4 + kp_cap * (8 + 6 + 128 + 360))
+
+    def run_batch(self, imgs: torch.Tensor):
+        """Detect + describe imgs uint8 [n, H, W] (n <= batch, device-resident, contiguous);
+        returns views kp_out [n, kp_cap, 6], desc [n, kp_cap, 128] and a contiguous copy of
+        the keypoint counts int32 [n] (all stream-ordered, no host sync)."""
+        if imgs.dtype != torch.uint8 or imgs.dim() != 3 or tuple(imgs.shape[1:]) != (self.H, self.W):
+            raise ValueError("SIFT input must be uint8 [n, H, W]")
+        n = int(imgs.shape[0])
+        if not 1 <= n <= self.batch:
+            raise ValueError(f"at most {self.batch} images per call")
+        imgs = imgs.to(self.device).contiguous()
+        st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        L.check(self.lib.vo_sift_batch(C.byref(self.sb), n, C.c_void_p(imgs.data_ptr()), self.W * self.H,
+                                       self.W, self.H, st), "vo_sift_batch")
+        self._img = imgs      # keep alive until the stream consumes it
+        return self.t["kp_out"][:n], self.t["desc"][:n], self.t["counters"][:n, 2].contiguous()
+
     def run(self, img: torch.Tensor):
-        """Detect + describe; results stay on the device (kp_out, desc, counters[2])."""
+        """Detect + describe one image; results stay on the device (kp_out, desc, count)."""
         if img.dtype != torch.uint8 or tuple(img.shape) != (self.H, self.W):
             raise ValueError("SIFT input must be uint8 [H, W]")
-        img = img.to(self.device).contiguous()
-        st = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        L.check(self.lib.vo_sift(C.byref(self.sb), C.c_void_p(img.data_ptr()), self.W, self.H, st), "vo_sift")
-        self._img = img      # keep alive until the stream consumes it
-        return self.t["kp_out"], self.t["desc"], self.t["counters"][2:3]
+        k, d, n = self.run_batch(img.reshape(1, self.H, self.W))
+        return k[0], d[0], n
 
-    def overflowed(self) -> bool:
-        return bool(int(self.t["counters"][3]))
+    def overflowed(self, n: int | None = None) -> bool:
+        c = self.t["counters"][: (n or 1), 3]
+        return bool(int(c.max()))
 
-    def result(self):
-        n = int(self.t["counters"][2])
-        if self.overflowed():
+    def result(self, b: int = 0):
+        n = int(self.t["counters"][b, 2])
+        if int(self.t["counters"][b, 3]):
             raise RuntimeError("SIFT capacity exceeded (raise cand_cap / kp_cap)")
-        return self.t["kp_out"][:n].cpu().numpy(), self.t["desc"][:n].cpu().numpy()
+        return self.t["kp_out"][b, :n].cpu().numpy(), self.t["desc"][b, :n].cpu().numpy()
 
 
 _SCRATCH: dict = {}

@@ -154,7 +154,7 @@ def _oracle_init(case):
     return g, fr, opts, boot, s
 
 
-@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3"])
+@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3", "malaga1024_c3"])
 def test_bootstrap_matches_oracle(case):
     from monocular_visual_odometry_va4mr_amd.VisualOdometryPipeLine import VisualOdometryPipeLine
     g, fr, opts, boot, s = _oracle_init(case)
@@ -173,7 +173,7 @@ def test_bootstrap_matches_oracle(case):
     assert np.array_equal(vo.outlier_pts_current, s.outl_pts)
 
 
-@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3"])
+@pytest.mark.parametrize("case", ["kitti_c2", "parking_c1", "malaga_c3", "malaga1024_c3"])
 def test_full_pipeline_ate_vs_reference(case):
     """Drop-in class on GPU vs the reference class's own run (golden fixture, produced by
     /root/reference/VisualOdometryPipeLine.py on the oracle primitives): every pose, every
@@ -207,3 +207,31 @@ def test_full_pipeline_ate_vs_reference(case):
     est = np.array([t.ravel() for _, t in tr])
     rmse, rel = ate(est, g["t"][:, :, 0])
     assert rel == 0.0 or rel < 1e-12
+
+
+def test_batched_bootstrap_matches_oracle_per_chain():
+    """Engine.bootstrap over 6 chains with the SIFT batch forced into chunks of 2 chains
+    (vo_sift_batch of 4 images, one batched BF launch and one ratio-match launch per chunk):
+    every chain's state is bit-identical to the oracle's initialization on its own pair."""
+    from oracle import vo_pipeline_oracle as V
+    from monocular_visual_odometry_va4mr_amd import options as Op
+    from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd.features import Sift
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    fr, K, _, _ = make_sequence("kitti", 14, seed=1)
+    opts, _, _ = Op.get("kitti")
+    starts = [0, 2, 4, 6, 8, 11]
+    eng = Engine(K, opts, 1241, 376, batch=len(starts), ncap=4096, pcap=8192, fcap=16)
+    eng.bootstrap(fr[starts], fr[[s + 2 for s in starts]], sift_batch_bytes=4 * Sift.bytes_per_image(1241, 376))
+    assert eng._sift.batch == 4
+    for b, s0 in enumerate(starts):
+        s = V.new_state(K, opts)
+        V.initialize(s, fr[s0], fr[s0 + 2])
+        e = eng.export_chain(b)
+        assert e["status"] == 0
+        R_g, t_g = e["transforms"][-1]
+        R_o, t_o = s.transforms[-1]
+        assert np.array_equal(R_g, R_o) and np.array_equal(t_g, t_o), f"chain {b}"
+        for name, ref in (("landmarks", s.lm), ("keypoints", s.kp), ("cand", s.cand),
+                          ("cand_first", s.cand_first), ("cand_tau", s.cand_tau)):
+            assert np.array_equal(e[name], ref), f"chain {b} {name}"

@@ -30,7 +30,8 @@ def _run_restatement(g, n_steps=None):
     return rows, snaps
 
 
-@pytest.mark.parametrize("case,n_steps", [("kitti_c2", None), ("parking_c1", 30), ("malaga_c3", None)])
+@pytest.mark.parametrize("case,n_steps", [("kitti_c2", 40), ("parking_c1", 30), ("malaga_c3", None),
+                                          ("malaga1024_c3", 12)])
 def test_restatement_matches_reference(case, n_steps):
     g = load_golden(case)
     rows, snaps = _run_restatement(g, n_steps)
@@ -49,7 +50,7 @@ def test_restatement_matches_reference(case, n_steps):
 
 def test_golden_sanity():
     """The recorded reference runs are non-degenerate (landmarks tracked, poses moving)."""
-    for case in ("parking_c1", "kitti_c2", "malaga_c3"):
+    for case in ("parking_c1", "kitti_c2", "malaga_c3", "malaga1024_c3"):
         g = load_golden(case)
         assert str(g["error"]) == ""
         assert (g["N"] >= 8).all()

@@ -42,7 +42,7 @@ def main():
         s0.run(a)
         s1.run(b)
         torch.cuda.synchronize()
-        res["keypoints"] = int(s0.t["counters"][2])
+        res["keypoints"] = int(s0.t["counters"][0, 2])
 
         def pair():
             k0, d0, n0 = s0.run(a)
