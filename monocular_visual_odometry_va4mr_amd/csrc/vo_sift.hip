@@ -78,18 +78,31 @@ VO_DEV float fast_atan2(float y, float x)
 // ------------------------------------------------------- per-image views
 // vo_sift_batch runs B images per launch: every buffer of vo_sift_buf holds B consecutive
 // per-image blocks of the size vo_sift_plan reports; blockIdx.z is the image.
-VO_DEV vo_sift_buf sift_img(vo_sift_buf sb, int z)
+// Per-image base pointers of image z.  The kernels keep the vo_sift_buf kernel argument
+// itself (offset tables indexed in kernarg memory) and address the data through these: a
+// modified local copy of the whole struct would be dynamically indexed, i.e. live in scratch.
+struct SiftImg {
+    float* gauss;
+    float* dog;
+    int32_t* counters;
+    int32_t* cand;
+    float* kp;
+    float* kp_out;
+    float* desc;
+    float* hist;
+};
+VO_DEV SiftImg sift_img(const vo_sift_buf& sb, int z)
 {
-    sb.gauss += (int64_t)z * sb.gauss_floats;
-    sb.dog += (int64_t)z * sb.dog_floats;
-    sb.tmp += (int64_t)z * sb.tmp_floats;
-    sb.counters += 8 * z;
-    sb.cand += (int64_t)z * sb.cand_cap * 4;
-    sb.kp += (int64_t)z * sb.kp_cap * 8;
-    sb.kp_out += (int64_t)z * sb.kp_cap * 6;
-    sb.desc += (int64_t)z * sb.kp_cap * 128;
-    sb.hist += (int64_t)z * sb.kp_cap * 360;
-    return sb;
+    SiftImg p;
+    p.gauss = sb.gauss + (int64_t)z * sb.gauss_floats;
+    p.dog = sb.dog + (int64_t)z * sb.dog_floats;
+    p.counters = sb.counters + 8 * z;
+    p.cand = sb.cand + (int64_t)z * sb.cand_cap * 4;
+    p.kp = sb.kp + (int64_t)z * sb.kp_cap * 8;
+    p.kp_out = sb.kp_out + (int64_t)z * sb.kp_cap * 6;
+    p.desc = sb.desc + (int64_t)z * sb.kp_cap * 128;
+    p.hist = sb.hist + (int64_t)z * sb.kp_cap * 360;
+    return p;
 }
 
 // ------------------------------------------------------- scale space
@@ -185,35 +198,44 @@ __global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* 
     dst[(int64_t)y * dw + x] = src[(int64_t)sy * sw + sx];
 }
 
-__global__ void k_extrema(vo_sift_buf sb_all, int o, int layer)
+__global__ void k_extrema(vo_sift_buf sb, int o, int layer)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     const int w = sb.oct_w[o], h = sb.oct_h[o];
     const int c = blockIdx.x * blockDim.x + threadIdx.x + SIFT_IMG_BORDER;
     const int r = blockIdx.y + SIFT_IMG_BORDER;
-    if (c >= w - SIFT_IMG_BORDER || r >= h - SIFT_IMG_BORDER) return;
-    const int idx = o * (N_LAYERS + 2) + layer;
-    const float* img = sb.dog + sb.dog_off[idx];
-    const float* prev = sb.dog + sb.dog_off[idx - 1];
-    const float* next = sb.dog + sb.dog_off[idx + 1];
-    const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
-    const float val = img[(int64_t)r * w + c];
-    if (!(fabsf(val) > threshold)) return;
-    bool ext = true;
-    for (int dz = 0; dz < 3 && ext; ++dz) {
-        const float* L = dz == 0 ? prev : (dz == 1 ? img : next);
-        for (int dy = -1; dy <= 1 && ext; ++dy)
-            for (int dx = -1; dx <= 1; ++dx) {
-                const float u = L[(int64_t)(r + dy) * w + (c + dx)];
-                if (val > 0 ? !(val >= u) : !(val <= u)) { ext = false; break; }
-            }
+    bool ext = c < w - SIFT_IMG_BORDER && r < h - SIFT_IMG_BORDER;
+    if (ext) {
+        const int idx = o * (N_LAYERS + 2) + layer;
+        const float* img = im.dog + sb.dog_off[idx];
+        const float* prev = im.dog + sb.dog_off[idx - 1];
+        const float* next = im.dog + sb.dog_off[idx + 1];
+        const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
+        const float val = img[(int64_t)r * w + c];
+        ext = fabsf(val) > threshold;
+        for (int dz = 0; dz < 3 && ext; ++dz) {
+            const float* L = dz == 0 ? prev : (dz == 1 ? img : next);
+            for (int dy = -1; dy <= 1 && ext; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const float u = L[(int64_t)(r + dy) * w + (c + dx)];
+                    if (val > 0 ? !(val >= u) : !(val <= u)) { ext = false; break; }
+                }
+        }
     }
+    // one atomic per wave: the list order is irrelevant (keypoints are canonically sorted)
+    const uint64_t m = __ballot(ext);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&im.counters[0], __popcll(m));
+    base = __shfl(base, leader, 64);
     if (!ext) return;
-    const int k = atomicAdd(&sb.counters[0], 1);
+    const int k = base + __popcll(m & ((1ull << lane) - 1ull));
     if (k < sb.cand_cap) {
-        sb.cand[4 * k] = o; sb.cand[4 * k + 1] = layer; sb.cand[4 * k + 2] = r; sb.cand[4 * k + 3] = c;
+        im.cand[4 * k] = o; im.cand[4 * k + 1] = layer; im.cand[4 * k + 2] = r; im.cand[4 * k + 3] = c;
     } else {
-        sb.counters[3] = 1;
+        im.counters[3] = 1;
     }
 }
 
@@ -249,7 +271,7 @@ VO_DEV void lu3_solve(float A[9], float b[3], float X[3])
 
 struct KP { float x, y, size, angle, response; int octave; };
 
-VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, KP& kpt, int octv, int& layer, int& r, int& c, float sigma)
+VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, const float* dogs, KP& kpt, int octv, int& layer, int& r, int& c, float sigma)
 {
     const float contrastThreshold = 0.04f, edgeThreshold = 10.f;
     const float img_scale = 1.f / (255 * 1);
@@ -261,9 +283,9 @@ VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, KP& kpt, int octv, int& 
     int i = 0;
     for (; i < SIFT_MAX_INTERP_STEPS; ++i) {
         const int idx = octv * (N_LAYERS + 2) + layer;
-        const float* img = sb.dog + sb.dog_off[idx];
-        const float* prev = sb.dog + sb.dog_off[idx - 1];
-        const float* next = sb.dog + sb.dog_off[idx + 1];
+        const float* img = dogs + sb.dog_off[idx];
+        const float* prev = dogs + sb.dog_off[idx - 1];
+        const float* next = dogs + sb.dog_off[idx + 1];
         float dD[3] = {(DAT(img, w, r, c + 1) - DAT(img, w, r, c - 1)) * deriv_scale,
                        (DAT(img, w, r + 1, c) - DAT(img, w, r - 1, c)) * deriv_scale,
                        (DAT(next, w, r, c) - DAT(prev, w, r, c)) * deriv_scale};
@@ -294,9 +316,9 @@ VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, KP& kpt, int octv, int& 
     if (i >= SIFT_MAX_INTERP_STEPS) return false;
     {
         const int idx = octv * (N_LAYERS + 2) + layer;
-        const float* img = sb.dog + sb.dog_off[idx];
-        const float* prev = sb.dog + sb.dog_off[idx - 1];
-        const float* next = sb.dog + sb.dog_off[idx + 1];
+        const float* img = dogs + sb.dog_off[idx];
+        const float* prev = dogs + sb.dog_off[idx - 1];
+        const float* next = dogs + sb.dog_off[idx + 1];
         float dD[3] = {(DAT(img, w, r, c + 1) - DAT(img, w, r, c - 1)) * deriv_scale,
                        (DAT(img, w, r + 1, c) - DAT(img, w, r - 1, c)) * deriv_scale,
                        (DAT(next, w, r, c) - DAT(prev, w, r, c)) * deriv_scale};
@@ -357,20 +379,20 @@ VO_DEV float orientation_hist(const float* img, int w, int h, int px, int py, in
     return maxval;
 }
 
-__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nc = min(sb.counters[0], sb.cand_cap);
+    const int nc = min(im.counters[0], sb.cand_cap);
     if (k >= nc) return;
     const float* tab = sb.consts + EXPTAB_OFF;
-    const int o = sb.cand[4 * k], i0 = sb.cand[4 * k + 1];
-    int r1 = sb.cand[4 * k + 2], c1 = sb.cand[4 * k + 3], layer = i0;
+    const int o = im.cand[4 * k], i0 = im.cand[4 * k + 1];
+    int r1 = im.cand[4 * k + 2], c1 = im.cand[4 * k + 3], layer = i0;
     KP kpt;
-    if (!adjust_local_extrema(sb, kpt, o, layer, r1, c1, 1.6f)) return;
+    if (!adjust_local_extrema(sb, im.dog, kpt, o, layer, r1, c1, 1.6f)) return;
     const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
     float hist[SIFT_ORI_HIST_BINS];
-    const float* g = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
+    const float* g = im.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
     const float omax = orientation_hist(g, sb.oct_w[o], sb.oct_h[o], c1, r1, __float2int_rn(SIFT_ORI_RADIUS * scl_octv),
                                         SIFT_ORI_SIG_FCTR * scl_octv, hist, tab);
     const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
@@ -383,13 +405,13 @@ __global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb_all)
             bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
             float angle = 360.f - (float)((360.f / n) * bin);
             if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-            const int q = atomicAdd(&sb.counters[1], 1);
+            const int q = atomicAdd(&im.counters[1], 1);
             if (q < sb.kp_cap) {
-                float* out = sb.kp + 8 * (int64_t)q;
+                float* out = im.kp + 8 * (int64_t)q;
                 out[0] = kpt.x; out[1] = kpt.y; out[2] = kpt.size; out[3] = angle; out[4] = kpt.response;
                 out[5] = __int_as_float(kpt.octave); out[6] = 0.f; out[7] = 0.f;
             } else {
-                sb.counters[3] = 1;
+                im.counters[3] = 1;
             }
         }
     }
@@ -406,45 +428,60 @@ __global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb_all)
 //                 (k_sift_kp's temphist[36] is indexed dynamically, i.e. lives in scratch.)
 //                 Keypoints are appended with atomics; k_sift_sort_dedupe orders them.
 #define SIFT_REC 12
-__global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nc = min(sb.counters[0], sb.cand_cap);
-    if (k >= nc) return;
-    const int o = sb.cand[4 * k], i0 = sb.cand[4 * k + 1];
-    int r1 = sb.cand[4 * k + 2], c1 = sb.cand[4 * k + 3], layer = i0;
+    const int nc = min(im.counters[0], sb.cand_cap);
+    if (blockIdx.x * blockDim.x >= nc) return;
+    int o = 0, r1 = 0, c1 = 0, layer = 0;
     KP kpt;
-    if (!adjust_local_extrema(sb, kpt, o, layer, r1, c1, 1.6f)) return;
+    bool ok = false;
+    if (k < nc) {
+        o = im.cand[4 * k];
+        layer = im.cand[4 * k + 1];
+        r1 = im.cand[4 * k + 2];
+        c1 = im.cand[4 * k + 3];
+        ok = adjust_local_extrema(sb, im.dog, kpt, o, layer, r1, c1, 1.6f);
+    }
+    // one atomic per wave (record order is irrelevant: keypoints are canonically sorted)
+    const uint64_t m = __ballot(ok);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&im.counters[4], __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (!ok) return;
     const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
-    const int q = atomicAdd(&sb.counters[4], 1);
-    if (q >= rec_cap) { sb.counters[3] = 1; return; }
-    float* rec = sb.hist + (int64_t)SIFT_REC * q;
+    const int q = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (q >= rec_cap) { im.counters[3] = 1; return; }
+    float* rec = im.hist + (int64_t)SIFT_REC * q;
     rec[0] = kpt.x; rec[1] = kpt.y; rec[2] = kpt.size; rec[3] = kpt.response;
     rec[4] = __int_as_float(kpt.octave); rec[5] = __int_as_float(o); rec[6] = __int_as_float(layer);
     rec[7] = __int_as_float(r1); rec[8] = __int_as_float(c1);
 }
 
-__global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pb_s4[4][16];
     __shared__ float4 pv_s4[4][16];
     __shared__ float th_s[4][SIFT_ORI_HIST_BINS + 4];
     __shared__ float hs_s[4][SIFT_ORI_HIST_BINS];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
-    const int n_rec = min(sb.counters[4], rec_cap);
+    const int n_rec = min(im.counters[4], rec_cap);
     for (int q = blockIdx.x * 4 + w; q < n_rec; q += gridDim.x * 4) {   // wave-uniform loop
         int* pbin = reinterpret_cast<int*>(pb_s4[w]);
         float* pval = reinterpret_cast<float*>(pv_s4[w]);
-        const float* rec = sb.hist + (int64_t)SIFT_REC * q;
+        const float* rec = im.hist + (int64_t)SIFT_REC * q;
         const float kx = rec[0], ky = rec[1], ksize = rec[2], kresp = rec[3];
         const int koct = __float_as_int(rec[4]), o = __float_as_int(rec[5]), layer = __float_as_int(rec[6]);
         const int py = __float_as_int(rec[7]), px = __float_as_int(rec[8]);
         const float* tab = sb.consts + EXPTAB_OFF;
         const float scl_octv = ksize * 0.5f / (float)(1 << o);
-        const float* img = sb.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
+        const float* img = im.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
         const int wd = sb.oct_w[o], ht = sb.oct_h[o];
         const int radius = __float2int_rn(SIFT_ORI_RADIUS * scl_octv);
         const float sigma = SIFT_ORI_SIG_FCTR * scl_octv;
@@ -529,13 +566,13 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb_all)
                 bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
                 float angle = 360.f - (float)((360.f / n) * bin);
                 if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-                const int qo = atomicAdd(&sb.counters[1], 1);
+                const int qo = atomicAdd(&im.counters[1], 1);
                 if (qo < sb.kp_cap) {
-                    float* out = sb.kp + 8 * (int64_t)qo;
+                    float* out = im.kp + 8 * (int64_t)qo;
                     out[0] = kx; out[1] = ky; out[2] = ksize; out[3] = angle; out[4] = kresp;
                     out[5] = __int_as_float(koct); out[6] = 0.f; out[7] = 0.f;
                 } else {
-                    sb.counters[3] = 1;
+                    im.counters[3] = 1;
                 }
             }
         }
@@ -557,14 +594,14 @@ VO_DEV bool kp_less(const float* a, const float* b)
 }
 
 #define SORT_N 16384
-__global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int idx[SORT_N];
     __shared__ int lds[16];
     const int tid = threadIdx.x;
-    const int n = min(sb.counters[1], sb.kp_cap);
-    if (n > SORT_N) { if (tid == 0) sb.counters[3] = 1; }
+    const int n = min(im.counters[1], sb.kp_cap);
+    if (n > SORT_N) { if (tid == 0) im.counters[3] = 1; }
     const int nn = n < SORT_N ? n : SORT_N;
     int P = 1;
     while (P < nn) P <<= 1;
@@ -581,7 +618,7 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb_all)
                 bool gt;
                 if (a < 0) gt = c >= 0;
                 else if (c < 0) gt = false;
-                else gt = kp_less(sb.kp + 8 * (int64_t)c, sb.kp + 8 * (int64_t)a);
+                else gt = kp_less(im.kp + 8 * (int64_t)c, im.kp + 8 * (int64_t)a);
                 if (gt == asc) { idx[lo] = c; idx[hi] = a; }
             }
             __syncthreads();
@@ -593,17 +630,17 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb_all)
         bool keep = false;
         const float* k = nullptr;
         if (i < nn) {
-            k = sb.kp + 8 * (int64_t)idx[i];
+            k = im.kp + 8 * (int64_t)idx[i];
             keep = true;
             if (i > 0) {
-                const float* p = sb.kp + 8 * (int64_t)idx[i - 1];
+                const float* p = im.kp + 8 * (int64_t)idx[i - 1];
                 keep = (k[0] != p[0] || k[1] != p[1] || k[2] != p[2] || k[3] != p[3]);
             }
         }
         int tot;
         const int pos = out + block_scan_flag(keep, lds, &tot);
         if (keep) {
-            float* o = sb.kp_out + 6 * (int64_t)pos;
+            float* o = im.kp_out + 6 * (int64_t)pos;
             int oct = __float_as_int(k[5]);
             oct = (oct & ~255) | ((oct - 1) & 255);                      // firstOctave = -1
             o[0] = k[0] * 0.5f; o[1] = k[1] * 0.5f; o[2] = k[2] * 0.5f; o[3] = k[3]; o[4] = k[4];
@@ -611,16 +648,16 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb_all)
         }
         out += tot;
     }
-    if (tid == 0) sb.counters[2] = out;
+    if (tid == 0) im.counters[2] = out;
 }
 
-__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= sb.counters[2]) return;
+    if (q >= im.counters[2]) return;
     const float* tab = sb.consts + EXPTAB_OFF;
-    const float* kp = sb.kp_out + 6 * (int64_t)q;
+    const float* kp = im.kp_out + 6 * (int64_t)q;
     const int kpo = (int)kp[5];
     int octave = kpo & 255, layer = (kpo >> 8) & 255;
     octave = octave < 128 ? octave : (-128 | octave);
@@ -628,7 +665,7 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
     const float size = kp[2] * scale;
     const float ptx = kp[0] * scale, pty = kp[1] * scale;
     const int oi = octave + 1;
-    const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
+    const float* img = im.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
     const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
     float angle = 360.f - kp[3];
     if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
@@ -645,7 +682,7 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
     if (radius > rmax) radius = rmax;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    float* hist = sb.hist + 360 * (int64_t)q;
+    float* hist = im.hist + 360 * (int64_t)q;
     for (int i = 0; i < (d + 2) * (d + 2) * (n + 2); ++i) hist[i] = 0.f;
     for (int i = -radius; i <= radius; ++i) {
         for (int j = -radius; j <= radius; ++j) {
@@ -684,7 +721,7 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
             hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
         }
     }
-    float* dst = sb.desc + 128 * (int64_t)q;
+    float* dst = im.desc + 128 * (int64_t)q;
     for (int i = 0; i < d; ++i)
         for (int j = 0; j < d; ++j) {
             const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
@@ -723,9 +760,9 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb_all)
 //  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
 #define SIFT_HITMASK ((1ull << 0) | (1ull << 1) | (1ull << 6) | (1ull << 7) | (1ull << 10) | (1ull << 11) | \
                       (1ull << 60) | (1ull << 61))
-__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb_all)
+__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
 {
-    const vo_sift_buf sb = sift_img(sb_all, blockIdx.z);
+    const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
     int (*pidx_s)[64] = reinterpret_cast<int (*)[64]>(pidx_s4);
     __shared__ float pval_s[4][64 * 8];
@@ -733,14 +770,14 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb_all)
     __shared__ float dst_s[4][128];
     __shared__ float red_s[4][2];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n_kp = sb.counters[2];
+    const int n_kp = im.counters[2];
     for (int q = blockIdx.x * 4 + w; q < n_kp; q += gridDim.x * 4) {     // wave-uniform loop
         int* pidx = pidx_s[w];
         float* pval = pval_s[w];
         float* hist = hist_s[w];
         float* dsl = dst_s[w];
         const float* tab = sb.consts + EXPTAB_OFF;
-        const float* kp = sb.kp_out + 6 * (int64_t)q;
+        const float* kp = im.kp_out + 6 * (int64_t)q;
         const int kpo = (int)kp[5];
         int octave = kpo & 255, layer = (kpo >> 8) & 255;
         octave = octave < 128 ? octave : (-128 | octave);
@@ -748,7 +785,7 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb_all)
         const float size = kp[2] * scale;
         const float ptx = kp[0] * scale, pty = kp[1] * scale;
         const int oi = octave + 1;
-        const float* img = sb.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
+        const float* img = im.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
         const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
         float angle = 360.f - kp[3];
         if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
@@ -887,7 +924,7 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb_all)
         const float thr = red_s[w][0];
         const float s2 = sqrtf(red_s[w][1]);
         const float nscale = SIFT_INT_DESCR_FCTR / (s2 > FLT_EPSILON ? s2 : FLT_EPSILON);
-        float* dst = sb.desc + 128 * (int64_t)q;
+        float* dst = im.desc + 128 * (int64_t)q;
         for (int t = lane; t < len; t += 64) {
             const float v = dsl[t] < thr ? dsl[t] : thr;
             const int iv = __float2int_rn(v * nscale);

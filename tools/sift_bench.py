@@ -29,7 +29,8 @@ def timed(fn, iters):
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    for preset in ("kitti", "malaga1024", "hd1080"):
+    presets = sys.argv[2].split(",") if len(sys.argv) > 2 else ("kitti", "malaga1024", "hd1080")
+    for preset in presets:
         fr, _, _, _ = make_sequence(preset, 2, seed=2)
         a = torch.from_numpy(np.ascontiguousarray(fr[0])).cuda()
         b = torch.from_numpy(np.ascontiguousarray(fr[1])).cuda()
@@ -50,6 +51,13 @@ def main():
             bf_knn2(d0, n0, d1, n1, d0.shape[0])
 
         res["ms_per_pair_sift_sift_match"] = round(timed(pair, iters), 3)
+        # batched: vo_sift_batch over nb images per launch sequence (the bootstrap's mode)
+        nb = 64 if preset != "hd1080" else 16
+        sb = Sift(a.shape[1], a.shape[0], "cuda", batch=nb)
+        imgs = torch.stack([a, b] * (nb // 2)).contiguous()
+        res[f"ms_per_image_batch{nb}"] = round(timed(lambda: sb.run_batch(imgs), max(1, iters // 2)) / nb, 4)
+        del sb
+        torch.cuda.empty_cache()
         print(json.dumps(res), flush=True)
 
 
