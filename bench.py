@@ -26,6 +26,9 @@ Extra JSON fields:
   cpu_baseline_threads -- the same restatement on up to 16 chains at once, one host thread
                   each: the multi-core CPU rate (aggregate frames/s)
   ate_vs_ref   -- ATE of the GPU trajectory vs that CPU run on the same frames
+  sequence     -- the whole 4541-frame sequence as 16 shards over the ranks, bootstrap
+                  included: frames/s = 4541 / wall, per-shard identity with the reference
+                  class's runs on the same shard boundaries, stitched ATE (sequence_leg)
 """
 from __future__ import annotations
 
@@ -75,6 +78,7 @@ def parse():
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (see profiles/)")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--no-match", action="store_true", help="skip the BF-matcher (MFMA) leg")
+    ap.add_argument("--no-sequence", action="store_true", help="skip the whole-sequence (16-shard) leg")
     ap.add_argument("--match-pairs", type=int, default=32, help="matcher leg: problems per launch")
     ap.add_argument("--match-n", type=int, default=8192, help="matcher leg: descriptors per image")
     return ap.parse_args()
@@ -233,6 +237,31 @@ def c5_leg(device, chains=64, steps=6, warmup=2):
             "track_roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(gbs / HBM_PEAK_GBS, 5)},
             "chains_ok": int((statuses == 0).sum())}
+
+
+def sequence_leg(device, seed, rank, world, n_shards=16):
+    """The whole C2 sequence as one job (sequence-level number): SEQ_LEN frames cut
+    into n_shards overlapping shards (30-frame overlap) spread over the ranks, bootstrap
+    included in the clock (frames pre-rendered into HBM), poses gathered to rank 0 and
+    stitched.  frames/s = SEQ_LEN / wall.  Every shard's trajectory is compared with the
+    reference class's own run on the same boundaries (tests/golden/kitti_seq00_shards.npz,
+    §8e), plus the stitched ATE against ground truth.  Run twice; the second run is reported."""
+    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
+    ref = reference_shards(os.path.join(ROOT, "tests", "golden", "kitti_seq00_shards.npz"), n_shards)
+    spr = max(1, n_shards // world)
+    res = None
+    for _ in range(2):
+        res = run("kitti", SEQ_LEN, spr, overlap=30, seed=seed, device=device, rank=rank, world=world,
+                  reference=ref, time_boot=False)
+    if res is None:
+        return None
+    st = res.get("stitched") or {}
+    return {"config": f"C2 whole sequence: {SEQ_LEN} frames as {res['shards']} overlapping shards on {world} GPU(s), "
+                      "bootstrap + every step timed, poses gathered + Sim(3)-stitched after",
+            "frames_per_s": res["sequence_frames_per_s"], "wall_s": res["wall_s"], "shards_ok": res["shards_ok"],
+            "failed_shards": res["failed_shards"], "vs_reference": res.get("vs_reference"),
+            "stitched_frames": st.get("frames"), "coverage_breaks": st.get("coverage_breaks"),
+            "stitched_ate_rel_vs_gt": st.get("ate_rel")}
 
 
 def cpu_baseline(K, opts, frames_np, gap):
@@ -447,6 +476,13 @@ def main():
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - t_g) * 1e3
 
+    seq = None
+    if not args.no_sequence:
+        try:                          # a secondary measurement never costs the headline line
+            seq = sequence_leg(device, args.seed, rank, world)
+        except Exception as exc:  # noqa: BLE001
+            seq = {"error": f"{type(exc).__name__}: {exc}"}
+
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -513,6 +549,8 @@ def main():
         "render_s": round(render_s, 2),
         "gather_ms": round(gather_ms, 3),
     }
+    if seq is not None:
+        out["sequence"] = seq
 
     if world == 1 and args.cpu_frames > 2 and not args.no_single:
         sample = render_windows(rend, gt, [0], gap, args.cpu_frames - 2, device)[:, 0]
