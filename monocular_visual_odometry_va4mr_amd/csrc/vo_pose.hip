@@ -665,6 +665,53 @@ __global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const 
 }
 
 // ------------------------------------------------------------------ triangulation
+// The reference forms its projection matrices and camera-frame depths with numpy
+// matmuls (VisualOdometryPipeLine.py:74-75 invert_transform, :157-168, :170-171), which
+// OpenBLAS evaluates as fused multiply-add chains whose order depends on the operands'
+// memory layout (tools/blas_order_probe.py checks the models below on the host):
+//   C-order matrix @ vector  (gemv, dot products)   fma(a2,b2, fma(a0,b0, a1*b1))
+//   F-order matrix @ vector  (gemv, column axpys)   fma(a2,b2, fma(a1,b1, a0*b0))
+//   K @ [R | t]              (gemm)                 fma(a2,b2, fma(a1,b1, a0*b0))
+// Every 3x3 gemm of check_baseline ((R_cur^T R_past)^T, then @ K_inv) is the k-order chain.
+// R_WC = R_CW.T is F-order for the identity pose 0 and the bootstrap pose 1 (recoverPose
+// returns a C-order R) and C-order for every later pose (R_CW = Rodrigues(rvec).T).  The
+// triangulated point depends on every bit of the two projection matrices, so they are
+// reproduced exactly; a landmark coordinate near 0 otherwise differs in its last float bit
+// (found 619 frames into the C2 chain, tools/diag_long.py).
+VO_DEV double dot_c012(const double* a, const double* b)
+{
+    return __builtin_fma(a[2], b[2], __builtin_fma(a[1], b[1], a[0] * b[0]));
+}
+VO_DEV double dot_c102(const double* a, const double* b)
+{
+    return __builtin_fma(a[2], b[2], __builtin_fma(a[0], b[0], a[1] * b[1]));
+}
+// (R_WC, t_WC) = invert_transform(R_CW, t_CW) of pose p: R_WC = R_CW^T, t_WC = (-R_WC) @ t_CW
+VO_DEV void pose_inverse(const double* Rcw, const double* tcw, int p, double* Rwc, double* twc)
+{
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Rwc[i * 3 + j] = Rcw[j * 3 + i];
+    for (int i = 0; i < 3; ++i) {
+        const double a[3] = {-Rwc[i * 3], -Rwc[i * 3 + 1], -Rwc[i * 3 + 2]};
+        twc[i] = p >= 2 ? dot_c102(a, tcw) : dot_c012(a, tcw);
+    }
+}
+// P = K @ np.hstack((R_WC, t_WC)), 3x4
+VO_DEV void proj_matrix(const double* K, const double* Rwc, const double* twc, double* P)
+{
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 4; ++j) {
+            const double m[3] = {j < 3 ? Rwc[j] : twc[0], j < 3 ? Rwc[3 + j] : twc[1], j < 3 ? Rwc[6 + j] : twc[2]};
+            P[i * 4 + j] = dot_c012(K + i * 3, m);
+        }
+}
+// z of (R_WC @ X + t_WC) (:157-168; X float32 promoted to float64)
+VO_DEV double depth_of(const double* Rwc, const double* twc, int p, const float* X)
+{
+    const double x[3] = {(double)X[0], (double)X[1], (double)X[2]};
+    return (p >= 2 ? dot_c102(Rwc + 6, x) : dot_c012(Rwc + 6, x)) + twc[2];
+}
+
 struct TriArgs {
     vo_dims d;
     vo_state s;
@@ -694,14 +741,8 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
         // current pose (R_CW, t_CW) is slot nF; (R_WC, t_WC) = (R^T, -R^T t)
         for (int i = 0; i < 9; ++i) Rc[i] = poseR[(int64_t)nF * 9 + i];
         for (int i = 0; i < 3; ++i) tc[i] = poset[(int64_t)nF * 3 + i];
-        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Rcwc[i * 3 + j] = Rc[j * 3 + i];
-        for (int i = 0; i < 3; ++i) tcwc[i] = -(Rcwc[i * 3] * tc[0] + Rcwc[i * 3 + 1] * tc[1] + Rcwc[i * 3 + 2] * tc[2]);
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 4; ++j) {
-                double acc = 0;
-                for (int q = 0; q < 3; ++q) acc += A.K[i * 3 + q] * (j < 3 ? Rcwc[q * 3 + j] : tcwc[q]);
-                Pc[i * 4 + j] = acc;
-            }
+        pose_inverse(Rc, tc, nF, Rcwc, tcwc);
+        proj_matrix(A.K, Rcwc, tcwc, Pc);
     }
     __syncthreads();
     float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
@@ -725,14 +766,17 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
                 const double* tp = poset + (int64_t)tau * 3;
                 // check_baseline :117-147: v_cur = K^-1 [u;1], v_past = ((R_cur^T R_past)^T K^-1) [u_f;1]
                 double vc[3], vp[3], rel[9], Mr[9];
-                for (int r = 0; r < 3; ++r) vc[r] = A.Kinv[r * 3] * (double)k0 + A.Kinv[r * 3 + 1] * (double)k1 + A.Kinv[r * 3 + 2];
+                const double uc[3] = {(double)k0, (double)k1, 1.0};
+                for (int r = 0; r < 3; ++r) vc[r] = dot_c102(A.Kinv + r * 3, uc);      // K_inv (C-order) @ v
                 for (int r = 0; r < 3; ++r)
                     for (int c = 0; c < 3; ++c)
-                        rel[c * 3 + r] = Rc[0 * 3 + r] * Rp[0 * 3 + c] + Rc[1 * 3 + r] * Rp[1 * 3 + c] + Rc[2 * 3 + r] * Rp[2 * 3 + c];
+                        rel[c * 3 + r] = __builtin_fma(Rc[6 + r], Rp[6 + c], __builtin_fma(Rc[3 + r], Rp[3 + c], Rc[r] * Rp[c]));
                 for (int r = 0; r < 3; ++r)
                     for (int c = 0; c < 3; ++c)
-                        Mr[r * 3 + c] = rel[r * 3] * A.Kinv[c] + rel[r * 3 + 1] * A.Kinv[3 + c] + rel[r * 3 + 2] * A.Kinv[6 + c];
-                for (int r = 0; r < 3; ++r) vp[r] = Mr[r * 3] * (double)f0 + Mr[r * 3 + 1] * (double)f1 + Mr[r * 3 + 2];
+                        Mr[r * 3 + c] = __builtin_fma(rel[r * 3 + 2], A.Kinv[6 + c],
+                                                      __builtin_fma(rel[r * 3 + 1], A.Kinv[3 + c], rel[r * 3] * A.Kinv[c]));
+                const double uf[3] = {(double)f0, (double)f1, 1.0};
+                for (int r = 0; r < 3; ++r) vp[r] = dot_c102(Mr + r * 3, uf);            // matmul output (C-order) @ v
                 double dot = vc[0] * vp[0] + vc[1] * vp[1] + vc[2] * vp[2];
                 double nc = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
                 double np = sqrt(vp[0] * vp[0] + vp[1] * vp[1] + vp[2] * vp[2]);
@@ -745,22 +789,16 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
                     retain = true;
                 } else {
                     double Rpw[9], tpw[3], Pp[12];
-                    for (int r = 0; r < 3; ++r) for (int c = 0; c < 3; ++c) Rpw[r * 3 + c] = Rp[c * 3 + r];
-                    for (int r = 0; r < 3; ++r) tpw[r] = -(Rpw[r * 3] * tp[0] + Rpw[r * 3 + 1] * tp[1] + Rpw[r * 3 + 2] * tp[2]);
-                    for (int r = 0; r < 3; ++r)
-                        for (int c = 0; c < 4; ++c) {
-                            double acc = 0;
-                            for (int q = 0; q < 3; ++q) acc += A.K[r * 3 + q] * (c < 3 ? Rpw[q * 3 + c] : tpw[q]);
-                            Pp[r * 4 + c] = acc;
-                        }
+                    pose_inverse(Rp, tp, tau, Rpw, tpw);
+                    proj_matrix(A.K, Rpw, tpw, Pp);
                     double X4[4];
                     tri_one(Pp, Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
                     const float w4 = (float)X4[3];
                     Xo[0] = (float)X4[0] / w4;
                     Xo[1] = (float)X4[1] / w4;
                     Xo[2] = (float)X4[2] / w4;
-                    const double zc = Rcwc[6] * (double)Xo[0] + Rcwc[7] * (double)Xo[1] + Rcwc[8] * (double)Xo[2] + tcwc[2];
-                    const double zp = Rpw[6] * (double)Xo[0] + Rpw[7] * (double)Xo[1] + Rpw[8] * (double)Xo[2] + tpw[2];
+                    const double zc = depth_of(Rcwc, tcwc, nF, Xo);
+                    const double zp = depth_of(Rpw, tpw, tau, Xo);
                     if (zc > A.min_d && zp > A.min_d && zc < A.max_d && zp < A.max_d) accept = true;
                     else retain = true;                               // quirk Q5
                 }
