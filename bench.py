@@ -518,6 +518,24 @@ def main():
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_by[dom], "mean_ms": round(dom_ms, 4)}
 
+    # k_lk_w is VALU-issue bound (profiles/*_sq.txt): achieved VALU wave-instructions/s from the
+    # profiled instructions per tracked point (profiles/lk_valu.json, rocprofv3 SQ_INSTS_VALU at
+    # the same config) x the points of this run / the live track time, against the CDNA4 issue
+    # peak (32-wide SIMDs: a wave64 VALU instruction every 2 cycles per SIMD)
+    roof_valu = None
+    vj = os.path.join(ROOT, "profiles", "lk_valu.json")
+    if os.path.exists(vj):
+        try:
+            with open(vj) as f:
+                vr = json.load(f)
+            peak_vi = 256 * 4 * 2.4e9 / 2
+            ach_vi = float(vr["valu_per_point"]) * npts / (dom_ms * 1e-3)
+            roof_valu = {"bound": "valu", "kernel": "k_lk_w", "achieved": round(ach_vi / 1e9, 2), "peak": peak_vi / 1e9,
+                         "unit": "G VALU wave-instr/s", "frac": round(ach_vi / peak_vi, 4),
+                         "valu_per_point": round(float(vr["valu_per_point"]), 1), "profile": vr.get("tag")}
+        except (OSError, ValueError, KeyError):
+            roof_valu = None
+
     out = {
         "metric": "frames/s + ATE vs ref, KITTI seq00 1241x376 @ 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -537,6 +555,7 @@ def main():
                    "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "seq_len": SEQ_LEN,
                    "seed": args.seed},
         "roofline": roof,
+        "roofline_valu": roof_valu,
         "stages_ms": stage,
         "chains_ok": n_ok_all,
         "chains_failed": world * B - n_ok_all,

@@ -821,6 +821,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const int iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
                 const int iw11 = (1 << 14) - iw00 - iw01 - iw10;
                 int ival[MAXJ], ixv[MAXJ], iyv[MAXJ];
+                // dot accumulator seed 256 - 512 * I: the iteration's (bilinear sum + 256) >> 9 - I
+                // becomes one arithmetic shift of the seeded sum (exact: the sum is >= 0 and
+                // 512 * I is a multiple of the shift; the int32 result is in range)
+                uint32_t iseed[MAXJ];
                 int a11 = 0, a12 = 0, a22 = 0;
                 // dI taps as int16 pairs against packed int16 weight pairs: two v_dot2_i32_i16
                 // per sum (exact: |dI| <= 4080, weights <= 2^14)
@@ -840,6 +844,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                                         __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x07060302u)), wp0,
                                                                1 << 13, false), false) >> 14;
                     ival[j] = live[j] ? v : 0;
+                    iseed[j] = 256u - ((uint32_t)ival[j] << 9);
                     ixv[j] = live[j] ? gx2 : 0;
                     iyv[j] = live[j] ? gy2 : 0;
                     a11 += __mul24(ixv[j], ixv[j]);
@@ -898,9 +903,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                         for (int j = 0; j < MAXJ; ++j) {
                             const uint32_t q = tb[toff[j]];
                             uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
-                                           __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                                           __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                             if (decltype(negc)::value) sum -= q >> 24;
-                            const int diff = (int)(sum >> 9) - ival[j];
+                            const int diff = (int)sum >> 9;
                             b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
                             b2 += __mul24(diff, iyv[j]);
                         }
@@ -955,9 +960,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     for (int j = 0; j < MAXJ; ++j) {
                         const uint32_t q = tb[toff[j]];
                         uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
-                                       __builtin_amdgcn_udot4(q, wlo, 256u, false);
+                                       __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                         if (neg) sum -= q >> 24;
-                        const int diff = (int)(sum >> 9) - ival[j];
+                        const int diff = (int)sum >> 9;
                         es += live[j] ? (diff < 0 ? -diff : diff) : 0;
                     }
                     errv = (float)wave_sum_dpp(es) / (float)(32 * WW * WH);
