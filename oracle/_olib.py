@@ -51,8 +51,16 @@ def _declare(L):
     L.vo_o_recover_pose.argtypes = [P, P, P, I, P, P, P, P, P]
     L.vo_o_sift.argtypes = [P, I, I, P, P, I, P]
     L.vo_o_bf_knn2.argtypes = [P, I, P, I, I, P, P]
+    L.vo_o_set_fp32_mode.argtypes = [I]
+    L.vo_o_set_fp32_mode.restype = None
     L.vo_o_rng_next.argtypes = [P]
     L.vo_o_rng_next.restype = C.c_uint32
+
+
+def set_fp32_mode(mode: int) -> None:
+    """0: integer-exact GFTT / LK sums (the parity oracle); bit 0: OpenCV-style fp32
+    cornerMinEigenVal; bit 1: LK sums in float (measurement only, see vo_oracle_img.c)."""
+    lib().vo_o_set_fp32_mode(int(mode))
 
 
 def ptr(a: np.ndarray | None):

@@ -12,6 +12,13 @@
  *     then larger address first) and the greedy grid test are OpenCV's.
  *   - LK: window sums A11/A12/A22/b1/b2 are accumulated exactly in int64 and
  *     converted to float once (OpenCV accumulates in fp32, lane-order dependent).
+ *
+ * vo_o_set_fp32_mode() switches on restatements of OpenCV's fp32 forms instead (never used
+ * by the parity tests; tools/opencv_fp32_sensitivity.py measures how often they change a
+ * result): bit 0 -- cornerMinEigenVal as Sobel * scale in float (scale on the smoothing
+ * taps), float covariance products, double box sums rounded to float, lambda in float
+ * (corner.cpp); bit 1 -- LK sums accumulated in float in raster order (lkpyramid.cpp's
+ * scalar loop).  OpenCV's SIMD builds may fuse and reorder these; unpinned either way.
  */
 #include "vo_oracle.h"
 
@@ -40,11 +47,61 @@ static inline int refl101(int p, int len)
     return p;
 }
 
+static int g_fp32_mode = 0;
+void vo_o_set_fp32_mode(int mode) { g_fp32_mode = mode; }
+
+/* OpenCV-style fp32 cornerMinEigenVal (bit 0 of the fp32 mode), blockSize x blockSize, ksize 3 */
+static int eigmap_fp32(const uint8_t* img, int w, int h, int bs, float* eig)
+{
+    size_t npx = (size_t)w * h;
+    float* cov = (float*)malloc(npx * 3 * sizeof(float));
+    if (!cov) return VO_O_EFAIL;
+    const double scale = 1.0 / ((double)(1 << 2) * bs * 255.0);
+    const float k0 = (float)(1.0 * scale), k1 = (float)(2.0 * scale);   /* smoothing taps * scale */
+    for (int y = 0; y < h; ++y) {
+        int ym = refl101(y - 1, h), yp = refl101(y + 1, h);
+        for (int x = 0; x < w; ++x) {
+            int xm = refl101(x - 1, w), xp = refl101(x + 1, w);
+            const uint8_t* r0 = img + (size_t)ym * w;
+            const uint8_t* r1 = img + (size_t)y * w;
+            const uint8_t* r2 = img + (size_t)yp * w;
+            /* dx: row difference, then the (1 2 1)*scale column pass; dy: row smoothing
+               (1 2 1) then the column difference, scaled by the smoothing taps */
+            float d0 = (float)(r0[xp] - r0[xm]), d1 = (float)(r1[xp] - r1[xm]), d2 = (float)(r2[xp] - r2[xm]);
+            float dxf = (d0 + d2) * k0 + d1 * k1;
+            float s0 = (float)r0[xm] * k0 + (float)r0[x] * k1 + (float)r0[xp] * k0;
+            float s2 = (float)r2[xm] * k0 + (float)r2[x] * k1 + (float)r2[xp] * k0;
+            float dyf = s2 - s0;
+            cov[3 * ((size_t)y * w + x)] = dxf * dxf;
+            cov[3 * ((size_t)y * w + x) + 1] = dxf * dyf;
+            cov[3 * ((size_t)y * w + x) + 2] = dyf * dyf;
+        }
+    }
+    int a0 = bs / 2;
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            double sa = 0, sb = 0, sc = 0;
+            for (int i = 0; i < bs; ++i) {
+                int yy = refl101(y - a0 + i, h);
+                for (int j = 0; j < bs; ++j) {
+                    int xx = refl101(x - a0 + j, w);
+                    const float* c = cov + 3 * ((size_t)yy * w + xx);
+                    sa += c[0]; sb += c[1]; sc += c[2];
+                }
+            }
+            float a = (float)sa * 0.5f, b = (float)sb, c = (float)sc * 0.5f;
+            eig[(size_t)y * w + x] = (float)((a + c) - sqrtf((a - c) * (a - c) + b * b));
+        }
+    free(cov);
+    return VO_O_OK;
+}
+
 /* ------------------------------------------------------------------ GFTT */
 int vo_o_eigmap(const uint8_t* img, int w, int h, int bs, int use_harris,
                 double harris_k, float* eig)
 {
     if (!img || w < 1 || h < 1 || bs < 1 || !eig) return VO_O_EARG;
+    if ((g_fp32_mode & 1) && !use_harris) return eigmap_fp32(img, w, h, bs, eig);
     size_t npx = (size_t)w * h;
     int32_t* dx = (int32_t*)malloc(npx * sizeof(int32_t));
     int32_t* dy = (int32_t*)malloc(npx * sizeof(int32_t));
@@ -387,6 +444,8 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
             int iw10 = (int)lrintf((1.f - a) * b * (1 << W_BITS));
             int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
             int64_t iA11 = 0, iA12 = 0, iA22 = 0;
+            float fA11 = 0.f, fA12 = 0.f, fA22 = 0.f;
+            const int lk32 = g_fp32_mode & 2;
             for (int y = 0; y < win_h; ++y) {
                 const uint8_t* src = I->img + (size_t)(y + ipy + I->by) * I->pw + (ipx + I->bx);
                 const int16_t* dsrc = I->der + ((size_t)(y + ipy + I->by) * I->pw + (ipx + I->bx)) * 2;
@@ -403,11 +462,14 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
                     iA11 += (int64_t)ixval * ixval;
                     iA12 += (int64_t)ixval * iyval;
                     iA22 += (int64_t)iyval * iyval;
+                    fA11 += (float)(ixval * ixval);
+                    fA12 += (float)(ixval * iyval);
+                    fA22 += (float)(iyval * iyval);
                 }
             }
-            float A11 = (float)iA11 * FLT_SCALE;
-            float A12 = (float)iA12 * FLT_SCALE;
-            float A22 = (float)iA22 * FLT_SCALE;
+            float A11 = (lk32 ? fA11 : (float)iA11) * FLT_SCALE;
+            float A12 = (lk32 ? fA12 : (float)iA12) * FLT_SCALE;
+            float A22 = (lk32 ? fA22 : (float)iA22) * FLT_SCALE;
             float D = A11 * A22 - A12 * A12;
             float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
                            (float)(2 * win_w * win_h);
@@ -432,6 +494,7 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
                 iw10 = (int)lrintf((1.f - a) * b * (1 << W_BITS));
                 iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
                 int64_t ib1 = 0, ib2 = 0;
+                float fb1 = 0.f, fb2 = 0.f;
                 for (int y = 0; y < win_h; ++y) {
                     const uint8_t* Jp = Jl->img + (size_t)(y + iny + Jl->by) * Jl->pw + (inx + Jl->bx);
                     for (int x = 0; x < win_w; ++x) {
@@ -439,10 +502,12 @@ int vo_o_lk(const uint8_t* prev, const uint8_t* next, int w, int h,
                                            Jp[x + Jl->pw + 1] * iw11, W_BITS - 5) - Iwin[y * win_w + x];
                         ib1 += (int64_t)diff * dIwin[2 * (y * win_w + x)];
                         ib2 += (int64_t)diff * dIwin[2 * (y * win_w + x) + 1];
+                        fb1 += (float)(diff * dIwin[2 * (y * win_w + x)]);
+                        fb2 += (float)(diff * dIwin[2 * (y * win_w + x) + 1]);
                     }
                 }
-                float b1 = (float)ib1 * FLT_SCALE;
-                float b2 = (float)ib2 * FLT_SCALE;
+                float b1 = (lk32 ? fb1 : (float)ib1) * FLT_SCALE;
+                float b2 = (lk32 ? fb2 : (float)ib2) * FLT_SCALE;
                 float ddx = (A12 * b2 - A22 * b1) * D;
                 float ddy = (A12 * b1 - A11 * b2) * D;
                 nx += ddx;

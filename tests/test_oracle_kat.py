@@ -29,13 +29,24 @@ def scene():
 
 
 def test_rng_matches_cv_rng():
+    """cv::RNG (operations.hpp: state = (uint64)(unsigned)state * 4164903690 + (state >> 32))
+    is a multiply-with-carry generator; with z = carry * 2^32 + x and p = a * 2^32 - 1 it
+    satisfies z_{n+1} = a * z_n (mod p) (a * 2^32 = 1 mod p), so after the first two draws
+    (which bring cv::RNG((uint64)-1)'s out-of-range initial carry into [0, p)) the n-th state
+    is 2^64 - 1 times a^n mod p: a closed form by modular exponentiation, checked against the
+    oracle's draws up to n = 20000 -- not a replay of the recurrence."""
     import ctypes
-    st = ctypes.c_uint64(0xFFFFFFFFFFFFFFFF)
-    s = 0xFFFFFFFFFFFFFFFF
-    for _ in range(100):
-        s = ((s & 0xFFFFFFFF) * 4164903690 + (s >> 32)) & 0xFFFFFFFFFFFFFFFF
+    a = 4164903690
+    p = a * 2 ** 32 - 1
+    z0 = 2 ** 64 - 1                         # RNG((uint64)-1), as solvePnPRansac / findEssentialMat seed it
+    st = ctypes.c_uint64(z0)
+    checks = {2, 3, 10, 100, 1000, 4096, 20000}
+    for n in range(1, 20001):
         v = O.lib().vo_o_rng_next(ctypes.byref(st))
-        assert v == (s & 0xFFFFFFFF)
+        if n in checks:
+            z = z0 * pow(a, n, p) % p
+            assert st.value == z, n
+            assert v == z % 2 ** 32, n
 
 
 def test_p3p_epnp_exact(scene):
