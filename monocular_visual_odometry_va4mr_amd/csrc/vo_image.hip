@@ -302,9 +302,9 @@ struct LKParams {
 // (hardware dispatch is round-robin over the 8 XCDs by linear block id), so the chain's
 // pyramid level stays in that XCD's 4 MB L2 instead of being fetched by all eight.
 // The mapping only affects speed; any block order gives the same results.
-VO_DEV bool lk_block(int B, int nb, int& b, int& pb, bool xcd = true)
+VO_DEV bool lk_block(int B, int nb, int& b, int& pb, bool xcd = true, int L = -1)
 {
-    const int L = blockIdx.x;
+    if (L < 0) L = blockIdx.x;
     if (B >= 8 && xcd) {
         const int xcd = L & 7, k = L >> 3;
         b = xcd + 8 * (k / nb);
@@ -610,8 +610,12 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // may run up to 3 bytes past a row end (next row, or the >= 64-byte tail slack that the
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
-template <int WW, int WH>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
+// WPB waves per block work as WPB independent one-wave blocks (own LDS slice, virtual block
+// index blockIdx.x * WPB + wave): with WPB = 4 a finished block frees four wave slots at once,
+// so the other stream group's 4-wave kernels (PnP, triangulation) are not starved of a CU by a
+// flood of single-wave LK blocks (VO_LK_WPB)
+template <int WW, int WH, int WPB>
+__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
 {
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
@@ -624,11 +628,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     static_assert(JRW >= QM + 1 && JRW <= JRS && IRW <= IRS && IRW <= 8 && DRW == 16 && QS % 4 == 0,
                   "k_lk_w staging layout");
     // one spare row in QT / IR / DR: read (never used) by the dead lanes of window row 15
-    __shared__ uint4 QT4[(TH + 1) * QM];
+    __shared__ uint4 QT4_all[WPB][(TH + 1) * QM];
+    __shared__ uint32_t JR_all[WPB][(TH + 1) * JRS];
+    __shared__ uint32_t IR_all[WPB][(WH + 2) * IRS];
+    __shared__ uint32_t DR_all[WPB][(WH + 2) * QS];
+    const int wv = WPB > 1 ? (int)(threadIdx.x >> 6) : 0;
+    uint4* QT4 = QT4_all[wv];
     const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
-    __shared__ uint32_t JR[(TH + 1) * JRS];
-    __shared__ uint32_t IR[(WH + 2) * IRS];
-    __shared__ uint32_t DR[(WH + 2) * QS];
+    uint32_t* JR = JR_all[wv];
+    uint32_t* IR = IR_all[wv];
+    uint32_t* DR = DR_all[wv];
     const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb, pcur = -1;
     const int lane = lane_id();
@@ -637,7 +646,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     for (level = level_hi; level >= level_lo; --level)
         for (int k = 2; k < 8; ++k) LKPROF_SET(k, 0);
     level = level_lo;
-    if (!lk_block(B, nb, b, pb, xcd != 0)) return;
+    if (!lk_block(B, nb, b, pb, xcd != 0, (int)blockIdx.x * WPB + wv)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
     const int n0 = P.n0 ? P.n0[b] : 0;
     int n1 = P.n1 ? P.n1[b] : 0;
@@ -2168,12 +2177,16 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
         hipLaunchKernelGGL(k_lk_q, dim3(B * nbq), dim3(64), 0, st, P, B, nbq);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
+    static const int wpb_env = [] { const char* e = getenv("VO_LK_WPB"); return e ? atoi(e) : 1; }();
     if (staged15 && fused_env) {
-        hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
+        if (wpb_env == 4 && nblk % 4 == 0)
+            hipLaunchKernelGGL((k_lk_w<15, 15, 4>), dim3(nblk / 4), dim3(256), 0, st, P, L, 0, B, nb, xcd_env);
+        else
+            hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {
-        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
+        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
         else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
         else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }
