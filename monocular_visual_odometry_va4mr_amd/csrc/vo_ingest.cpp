@@ -5,8 +5,11 @@
 //
 // PNG: 8-bit gray / gray+alpha / RGB / RGBA / palette, non-interlaced, all five row filters.
 // Colour images become gray the way OpenCV's PNG decoder asks libpng to do it
-// (png_set_rgb_to_gray(1, 0.299, 0.587): 15-bit fixed-point coefficients 9798 / 19235 / 3735,
-// rounding by +2^14) -- restated, parity with libpng unpinned (no OpenCV/libpng headers here).
+// (png_set_rgb_to_gray(1, 0.299, 0.587)), restated from libpng 1.6's integer path without
+// gamma: the weights are fixed to 1e-5 units (29900, 58700) and scaled to 15 bits by
+// truncation, (w * 32768) / 100000 -> red 9797, green 19234, blue 32768 - red - green = 3737;
+// a pixel is (rc*R + gc*G + bc*B) >> 15 (truncating), and a pixel with R == G == B is passed
+// through unchanged.  Parity with libpng / OpenCV unpinned (neither is in this image).
 // 16-bit images keep the high byte (png_set_strip_16).
 #include <stdint.h>
 #include <stdio.h>
@@ -64,9 +67,13 @@ int paeth(int a, int b, int c)
     return pb <= pc ? b : c;
 }
 
+constexpr int GRAY_RC = (29900 * 32768) / 100000;             // 9797
+constexpr int GRAY_GC = (58700 * 32768) / 100000;             // 19234
+constexpr int GRAY_BC = 32768 - GRAY_RC - GRAY_GC;            // 3737
 inline uint8_t rgb_to_gray(int r, int g, int b)
 {
-    return (uint8_t)((9798 * r + 19235 * g + 3735 * b + 16384) >> 15);
+    if (r == g && r == b) return (uint8_t)r;
+    return (uint8_t)((GRAY_RC * r + GRAY_GC * g + GRAY_BC * b) >> 15);
 }
 
 int decode_png(const uint8_t* d, size_t n, uint8_t* out, int64_t pitch, int want_w, int want_h)

@@ -8,8 +8,15 @@ PIL = pytest.importorskip("PIL.Image")
 
 
 def _gray_ref(rgb):
+    """libpng 1.6 png_set_rgb_to_gray(1, 0.299, 0.587) without gamma (OpenCV's IMREAD_GRAYSCALE
+    path for colour PNGs): truncated 15-bit weights 9797 / 19234 / 3737, truncating shift,
+    gray pixels passed through (parity with libpng itself unpinned: it is not in this image)."""
     rgb = rgb.astype(np.int64)
-    return ((9798 * rgb[..., 0] + 19235 * rgb[..., 1] + 3735 * rgb[..., 2] + 16384) >> 15).astype(np.uint8)
+    rc, gc = (29900 * 32768) // 100000, (58700 * 32768) // 100000
+    bc = 32768 - rc - gc
+    g = (rc * rgb[..., 0] + gc * rgb[..., 1] + bc * rgb[..., 2]) >> 15
+    same = (rgb[..., 0] == rgb[..., 1]) & (rgb[..., 0] == rgb[..., 2])
+    return np.where(same, rgb[..., 0], g).astype(np.uint8)
 
 
 @pytest.fixture(scope="module")
