@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stagger", type=int, default=0, help="1: start the groups out of phase (see main)")
+    ap.add_argument("--cu-reserve", type=int, default=int(os.environ.get("VO_CU_RESERVE", "0")),
+                    help="launch LK on a CU-masked stream per group that leaves this many CUs free "
+                         "for the other groups' latency-bound stages (0: off)")
     ap.add_argument("--prio", default="none", choices=["none", "g0", "side"], help="HIP stream priorities of the groups")
     ap.add_argument("--cpu-threads", type=int, default=16, help="chains (processes) in the all-cores CPU leg (1: skip)")
     ap.add_argument("--cpu-mt-frames", type=int, default=30, help="steps per chain in the multi-thread CPU leg")
@@ -399,6 +402,9 @@ def main():
         hi = args.prio == "g0" and g == 0 and G > 1
         engines[-1].side_priority = -1 if (hi or args.prio == "side") else 0
         streams.append(torch.cuda.Stream(device, priority=-1 if hi else 0) if G > 1 else torch.cuda.current_stream(device))
+        if args.cu_reserve > 0 and G > 1:
+            from monocular_visual_odometry_va4mr_amd.engine import cu_masked_stream
+            engines[-1].bulk_stream, _h = cu_masked_stream(device, args.cu_reserve)
     eng = engines[0]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -559,7 +565,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": "C2 kitti seq00-length synthetic 1241x376, per-frame continuous_operation",
                    "width": Wd, "height": H, "chains_per_gpu": B, "frames_per_step": world * B,
-                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "seq_len": SEQ_LEN,
+                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "cu_reserve": args.cu_reserve, "seq_len": SEQ_LEN,
                    "seed": args.seed},
         "roofline": roof,
         "roofline_valu": roof_valu,

@@ -125,6 +125,11 @@ typedef struct vo_state {
 /* ---- library ---------------------------------------------------------------- */
 const char* vo_version(void);
 int vo_device_arch(char* buf, int len);          /* gcnArchName of the current device */
+int vo_device_cus(void);                          /* compute units of the current device (or < 0) */
+/* Runtime helpers (no reference counterpart): a HIP stream restricted to the CUs whose bits
+ * are set in mask[nwords] (bit i of word i/32 = CU i), and its release. */
+int vo_stream_create_cumask(int nwords, const uint32_t* mask, vo_stream_t* out);
+int vo_stream_destroy(vo_stream_t s);
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 

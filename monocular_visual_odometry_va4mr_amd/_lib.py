@@ -127,6 +127,9 @@ def _declare(L):
     sig = {
         "vo_version": ([], C.c_char_p),
         "vo_device_arch": ([C.c_char_p, C.c_int], C.c_int),
+        "vo_device_cus": ([], C.c_int),
+        "vo_stream_create_cumask": ([C.c_int, P, P], C.c_int),
+        "vo_stream_destroy": ([P], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),

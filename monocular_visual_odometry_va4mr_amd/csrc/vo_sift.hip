@@ -758,6 +758,33 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
 //    contribution that lands in its bins (0 elsewhere, which leaves a register unchanged):
 //    each bin receives its additions in exactly the serial order;
 //  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
+// LDS float add without return (ds_add_f32).  Written as asm so that no lgkmcnt wait is put
+// before each one (the compiler cannot see them): a wave's LDS operations execute in issue order, so later LDS reads of the
+// same bins see every add, and there is no returned data to wait for.
+// hist[p] += v for the lanes in `lanes` (wave-uniform): plain LDS read, v_add_f32, write.
+VO_DEV void lds_rmw_add_lanes(float* p, float v, uint64_t lanes)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
+    uint64_t save;
+    float h;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %4\n\tds_read_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\t"
+                 "v_add_f32 %1, %1, %3\n\tds_write_b32 %2, %1\n\ts_mov_b64 exec, %0"
+                 : "=&s"(save), "=&v"(h)
+                 : "v"(a), "v"(v), "s"(lanes)
+                 : "memory");
+}
+
+// Only the lanes in `lanes` (wave-uniform) add: exec is narrowed and restored in the asm.
+VO_DEV void lds_add_f32_lanes(float* p, float v, uint64_t lanes)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
+    uint64_t save;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %3\n\tds_add_f32 %1, %2\n\ts_mov_b64 exec, %0"
+                 : "=&s"(save)
+                 : "v"(a), "v"(v), "s"(lanes)
+                 : "memory");
+}
+
 #define SIFT_HITMASK ((1ull << 0) | (1ull << 1) | (1ull << 6) | (1ull << 7) | (1ull << 10) | (1ull << 11) | \
                       (1ull << 60) | (1ull << 61))
 __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
@@ -804,7 +831,7 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
         sin_t /= hist_width;
         const int side = 2 * radius + 1;
         const int total = side * side;
-        float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, h4 = 0.f, h5 = 0.f;
+        for (int t = lane; t < 384; t += 64) hist[t] = 0.f;
         for (int base = 0; base < total; base += 64) {
             const int pos = base + lane;
             bool valid = false;
@@ -854,45 +881,26 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // four pixels per step: their LDS reads are issued together, the additions stay in
-            // pixel order (pidx is padded to a multiple of 4 with a bin no lane owns... see below)
-            for (int p0 = 0; p0 < nv; p0 += 4) {
-                const int4 ids = *reinterpret_cast<const int4*>(pidx + p0);
-                const int idv[4] = {ids.x, ids.y, ids.z, ids.w};
-                float vv4[4];
-                int kk4[4];
+            // walk the valid pixels in raster order, 8 at a time: lane 8*j + k holds pixel
+            // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so one LDS float
+            // add (ds_add_f32, eight lanes) applies them, and the wave's LDS operations execute
+            // in issue order -- every bin receives its additions in exactly the serial order
+            for (int g = 0; g < nv; g += 8) {
+                const int s = g + (lane >> 3), k = lane & 7;
+                const bool act = s < nv;
+                const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
+                const int addr = act ? pidx[s] + koff : 0;
+                const float v = act ? pval[g * 8 + lane] : 0.f;
+                // pixel j's eight lanes read their bins, add, write back; the next pixel's
+                // read is issued after this write (a wave's LDS operations execute in order)
+                const uint64_t am = __ballot(act);
     #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int id = idv[u];
-                    const int off = (lane - id) & 63;
-                    const bool hit = p0 + u < nv && ((SIFT_HITMASK >> off) & 1ull);
-                    // off -> slot: 0,1 -> 0,1; 10,11 -> 2,3; 60,61 -> 4,5; 6,7 (70,71 mod 64) -> 6,7
-                    const int sl = (off & 1) | (off >= 60 ? 4 : (off >= 10 ? 2 : (off >= 6 ? 6 : 0)));
-                    vv4[u] = hit ? pval[(p0 + u) * 8 + sl] : 0.f;
-                    const int real = off + (off == 6 || off == 7 ? 64 : 0);
-                    kk4[u] = (id + real - lane) >> 6;
-                }
-    #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float v = vv4[u];
-                    const int k = kk4[u];
-                    h0 += k == 0 ? v : 0.f;
-                    h1 += k == 1 ? v : 0.f;
-                    h2 += k == 2 ? v : 0.f;
-                    h3 += k == 3 ? v : 0.f;
-                    h4 += k == 4 ? v : 0.f;
-                    h5 += k == 5 ? v : 0.f;
-                }
+                for (int j = 0; j < 8; ++j) lds_rmw_add_lanes(hist + addr, v, am & (0xFFull << (8 * j)));
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        hist[lane] = h0; hist[lane + 64] = h1; hist[lane + 128] = h2;
-        hist[lane + 192] = h3; hist[lane + 256] = h4; hist[lane + 320] = h5;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // circular orientation wrap + copy (independent per output)
         for (int t = lane; t < d * d * n; t += 64) {
             const int cell = t / n, k = t - cell * n;

@@ -266,7 +266,15 @@ class Engine:
         if forked:
             side.wait_stream(main)                                # pyramid(cur) ready
         run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
-        run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
+        bulk = getattr(self, "bulk_stream", None)
+        if bulk is not None:
+            # LK on a CU-masked stream (set by the caller, see cu_masked_stream)
+            sb = C.c_void_p(bulk.cuda_stream)
+            bulk.wait_stream(main)
+            run(1, bulk, lambda: lib.vo_track(pd, po, ps, prev, sb))
+            main.wait_stream(bulk)
+        else:
+            run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
         run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
         run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
         if forked:
@@ -436,3 +444,36 @@ class Engine:
         planes = [t[q * d.pyr_stride + o:q * d.pyr_stride + o + n].view(h + 2 * L.VO_BORDER, p) for q in (0, 1)]
         buf = torch.stack(planes, dim=-1)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()
+
+
+def reserve_mask(n_cus: int, reserve: int) -> list:
+    """CU-mask words with `reserve` CUs cleared, spread evenly over the XCDs whether the
+    driver numbers CUs XCD-contiguously (CU i on XCD i // (n/8)) or round-robin (XCD i % 8):
+    the cleared CUs are 33*j + 8*m (j = 0..7, m = 0..reserve/8-1) for 256 CUs."""
+    bits = [1] * n_cus
+    per = max(1, reserve // 8)
+    for j in range(8):
+        for m in range(per):
+            i = (n_cus // 8 + 1) * j + 8 * m
+            if i < n_cus:
+                bits[i] = 0
+    words = [0] * ((n_cus + 31) // 32)
+    for i, b in enumerate(bits):
+        if b:
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def cu_masked_stream(device, reserve: int):
+    """A torch stream (wrapping a HIP stream from vo_stream_create_cumask) that launches on
+    every CU but `reserve` of them; returns (stream, handle) -- release with
+    lib().vo_stream_destroy(handle) after the last use."""
+    lib = L.lib()
+    n = lib.vo_device_cus()
+    if n <= 0:
+        raise RuntimeError("vo_device_cus failed")
+    words = reserve_mask(n, reserve)
+    arr = (C.c_uint32 * len(words))(*words)
+    h = C.c_void_p()
+    L.check(lib.vo_stream_create_cumask(len(words), arr, C.byref(h)), "vo_stream_create_cumask")
+    return torch.cuda.ExternalStream(h.value, device=device), h
