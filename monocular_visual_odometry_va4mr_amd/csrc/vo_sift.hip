@@ -147,39 +147,68 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
                                                    float* __restrict__ dog, int64_t dog_stride, int w, int h,
                                                    const float* __restrict__ kern, int n)
 {
-    __shared__ float s_src[(BT_H + 2 * BT_R) * (BT_W + 2 * BT_R)];
-    __shared__ float s_row[(BT_H + 2 * BT_R) * BT_W];
+    // LDS sized by the host for this kernel's radius (blur_lds): more blocks per CU for the
+    // small kernels
+    extern __shared__ float s_dyn[];
     __shared__ float s_k[2 * BT_R + 1];
     const int tid = threadIdx.x;
     const int r = n >> 1;
+    float* s_src = s_dyn;
+    float* s_row = s_dyn + (BT_H + 2 * r) * (BT_W + 2 * r);
     const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
     src += blockIdx.z * src_stride;
     dst += blockIdx.z * dst_stride;
     if (tid < n) s_k[tid] = kern[tid];
     const int rows = BT_H + 2 * r, cols = BT_W + 2 * r;
-    for (int i = tid; i < rows * cols; i += 256) {
-        const int ty = i / cols, tx = i - ty * cols;
-        const int gy = refl101(y0 - r + ty, h), gx = refl101(x0 - r + tx, w);
-        s_src[i] = src[(int64_t)gy * w + gx];
+    // staging: 64 lanes along a row, the four waves on rows w, w+4, ... (reflection computed per
+    // row / column, no division per element)
+    {
+        const int lx = tid & 63, wy = tid >> 6;
+        for (int ty = wy; ty < rows; ty += 4) {
+            const float* srow = src + (int64_t)refl101(y0 - r + ty, h) * w;
+            for (int tx = lx; tx < cols; tx += 64) s_src[ty * cols + tx] = srow[refl101(x0 - r + tx, w)];
+        }
     }
     __syncthreads();
-    for (int i = tid; i < rows * BT_W; i += 256) {
-        const int ty = i >> 6, tx = i & (BT_W - 1);
+    // row pass: four adjacent outputs per thread share one sliding window of n + 3 reads; each
+    // output still sums its taps k = 0..n-1 in order
+    for (int i = tid; i < rows * (BT_W / 4); i += 256) {
+        const int ty = i >> 4, tx = (i & 15) * 4;
         const float* sp = s_src + ty * cols + tx;
-        float acc = 0.f;
-        for (int k = 0; k < n; ++k) acc += s_k[k] * sp[k];
-        s_row[i] = acc;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        float v0 = sp[0], v1 = sp[1], v2 = sp[2];
+        for (int k = 0; k < n; ++k) {
+            const float v3 = sp[k + 3], kk = s_k[k];
+            a0 += kk * v0; a1 += kk * v1; a2 += kk * v2; a3 += kk * v3;
+            v0 = v1; v1 = v2; v2 = v3;
+        }
+        *reinterpret_cast<float4*>(s_row + ty * BT_W + tx) = make_float4(a0, a1, a2, a3);
     }
     __syncthreads();
-    for (int i = tid; i < BT_H * BT_W; i += 256) {
-        const int ty = i >> 6, tx = i & (BT_W - 1);
-        const int gy = y0 + ty, gx = x0 + tx;
-        if (gy >= h || gx >= w) continue;
-        const float* sp = s_row + ty * BT_W + tx;
-        float acc = 0.f;
-        for (int k = 0; k < n; ++k) acc += s_k[k] * sp[k * BT_W];
-        dst[(int64_t)gy * w + gx] = acc;
-        if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc - s_src[(ty + r) * cols + tx + r];
+    // column pass: four rows per thread (rows q, q + 8, q + 16, q + 24 would not share reads;
+    // adjacent rows do)
+    {
+        const int tx = tid & 63, ty = (tid >> 6) * 8;
+        const int gx = x0 + tx;
+        for (int half = 0; half < 2; ++half) {
+            const int tyh = ty + 4 * half;
+            const float* sp = s_row + tyh * BT_W + tx;
+            float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            float v0 = sp[0], v1 = sp[BT_W], v2 = sp[2 * BT_W];
+            for (int k = 0; k < n; ++k) {
+                const float v3 = sp[(k + 3) * BT_W], kk = s_k[k];
+                a0 += kk * v0; a1 += kk * v1; a2 += kk * v2; a3 += kk * v3;
+                v0 = v1; v1 = v2; v2 = v3;
+            }
+            const float acc[4] = {a0, a1, a2, a3};
+    #pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int gy = y0 + tyh + j;
+                if (gy >= h || gx >= w) continue;
+                dst[(int64_t)gy * w + gx] = acc[j];
+                if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc[j] - s_src[(tyh + j + r) * cols + tx + r];
+            }
+        }
     }
 }
 
@@ -236,6 +265,73 @@ __global__ void k_extrema(vo_sift_buf sb, int o, int layer)
         im.cand[4 * k] = o; im.cand[4 * k + 1] = layer; im.cand[4 * k + 2] = r; im.cand[4 * k + 3] = c;
     } else {
         im.counters[3] = 1;
+    }
+}
+
+// All three extremum layers of one octave from one LDS tile: 64 x 16 interior pixels per
+// block, the five DoG layers of the octave with a 1-pixel halo staged once; each pixel that
+// passes the threshold is compared with the max / min of its 3x3x3 neighbourhood (all 27 reads
+// independent, no early exit -- the per-pixel loop with an exit at the first failing neighbour
+// was a chain of dependent global loads).  The test is findScaleSpaceExtrema's:
+// val > 0 && val >= every neighbour, or val < 0 && val <= every neighbour (the centre itself is
+// one of the 27, which changes nothing).  Candidates are appended with one atomic per wave; the
+// list order is irrelevant (keypoints are sorted canonically).
+#define EX_W 64
+#define EX_H 16
+__global__ void __launch_bounds__(256) k_extrema_t(vo_sift_buf sb, int o)
+{
+    const SiftImg im = sift_img(sb, blockIdx.z);
+    __shared__ float t[N_LAYERS + 2][EX_H + 2][EX_W + 2];
+    const int w = sb.oct_w[o], h = sb.oct_h[o];
+    const int x0 = SIFT_IMG_BORDER + blockIdx.x * EX_W, y0 = SIFT_IMG_BORDER + blockIdx.y * EX_H;
+    const int tid = threadIdx.x;
+    const float* dog0 = im.dog + sb.dog_off[o * (N_LAYERS + 2)];
+    const int64_t plane = (int64_t)w * h;               // the octave's DoG layers are contiguous
+    for (int i = tid; i < (N_LAYERS + 2) * (EX_H + 2) * (EX_W + 2); i += 256) {
+        const int l = i / ((EX_H + 2) * (EX_W + 2));
+        const int rem = i - l * (EX_H + 2) * (EX_W + 2);
+        const int ty = rem / (EX_W + 2), tx = rem - ty * (EX_W + 2);
+        const int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
+        t[l][ty][tx] = (gy < h && gx < w) ? dog0[l * plane + (int64_t)gy * w + gx] : 0.f;
+    }
+    __syncthreads();
+    const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
+    const int tx = tid & (EX_W - 1), ty0 = (tid >> 6) * (EX_H / 4);
+    const int c = x0 + tx;
+    const int lane = tid & 63;
+    for (int layer = 1; layer <= N_LAYERS; ++layer) {
+        for (int k = 0; k < EX_H / 4; ++k) {
+            const int ty = ty0 + k, r = y0 + ty;
+            const float val = t[layer][ty + 1][tx + 1];
+            bool ext = c < w - SIFT_IMG_BORDER && r < h - SIFT_IMG_BORDER && fabsf(val) > threshold;
+            if (ext) {
+                float mx = val, mn = val;
+    #pragma unroll
+                for (int dz = -1; dz <= 1; ++dz)
+    #pragma unroll
+                    for (int dy = 0; dy < 3; ++dy)
+    #pragma unroll
+                        for (int dx = 0; dx < 3; ++dx) {
+                            const float u = t[layer + dz][ty + dy][tx + dx];
+                            mx = fmaxf(mx, u);
+                            mn = fminf(mn, u);
+                        }
+                ext = val > 0 ? val >= mx : val <= mn;
+            }
+            const uint64_t m = __ballot(ext);
+            if (m == 0) continue;
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(&im.counters[0], __popcll(m));
+            base = __shfl(base, leader, 64);
+            if (!ext) continue;
+            const int q = base + __popcll(m & ((1ull << lane) - 1ull));
+            if (q < sb.cand_cap) {
+                im.cand[4 * q] = o; im.cand[4 * q + 1] = layer; im.cand[4 * q + 2] = r; im.cand[4 * q + 3] = c;
+            } else {
+                im.counters[3] = 1;
+            }
+        }
     }
 }
 
@@ -774,7 +870,7 @@ VO_DEV void lds_rmw_add_lanes(float* p, float v, uint64_t lanes)
                  : "memory");
 }
 
-__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_sift_desc_w(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
@@ -821,57 +917,49 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
         for (int t = lane; t < 384; t += 64) hist[t] = 0.f;
         for (int base = 0; base < total; base += 64) {
             const int pos = base + lane;
-            bool valid = false;
-            int idx = 0;
-            float vv[8];
-            if (pos < total) {
-                const int ii = pos / side;
-                const int i = ii - radius, j = pos - ii * side - radius;
-                const float c_rot = j * cos_t - i * sin_t;
-                const float r_rot = j * sin_t + i * cos_t;
-                float rbin = r_rot + d / 2 - 0.5f;
-                float cbin = c_rot + d / 2 - 0.5f;
-                const int r = ptiy + i, c = ptix + j;
-                valid = rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1;
-                if (valid) {
-                    const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
-                    const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
-                    const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
-                    const float o = fast_atan2(dy, dx);
-                    const float mag = sqrtf(dx * dx + dy * dy) * wgt;
-                    float obin = (o - ori) * bins_per_rad;
-                    int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
-                    rbin -= r0; cbin -= c0; obin -= o0;
-                    if (o0 < 0) o0 += n;
-                    if (o0 >= n) o0 -= n;
-                    const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                    const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                    const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                    const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                    const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                    const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                    const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                    idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-                    // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
-                    vv[0] = v_rco000; vv[1] = v_rco001; vv[2] = v_rco010; vv[3] = v_rco011;
-                    vv[4] = v_rco100; vv[5] = v_rco101; vv[6] = v_rco110; vv[7] = v_rco111;
-                }
-            }
+            const int ii = pos / side;
+            const int i = ii - radius, j = pos - ii * side - radius;
+            const float c_rot = j * cos_t - i * sin_t;
+            const float r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + d / 2 - 0.5f;
+            float cbin = c_rot + d / 2 - 0.5f;
+            const int r = ptiy + i, c = ptix + j;
+            const bool valid = pos < total && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 &&
+                               c > 0 && c < cols - 1;
+            // compaction slot first, so each contribution goes to LDS as soon as it is formed
             const uint64_t m = __ballot(valid);
             const int nv = __popcll(m);
             if (valid) {
                 const int slot = __popcll(m & ((1ull << lane) - 1ull));
-                pidx[slot] = idx;
-    #pragma unroll
-                for (int k = 0; k < 8; ++k) pval[slot * 8 + k] = vv[k];
+                float* pv = pval + slot * 8;
+                const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
+                const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
+                const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
+                const float o = fast_atan2(dy, dx);
+                const float mag = sqrtf(dx * dx + dy * dy) * wgt;
+                float obin = (o - ori) * bins_per_rad;
+                int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
+                rbin -= r0; cbin -= c0; obin -= o0;
+                if (o0 < 0) o0 += n;
+                if (o0 >= n) o0 -= n;
+                pidx[slot] = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+                // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
+                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                pv[0] = v_rco000; pv[1] = v_rco001; pv[2] = v_rco010; pv[3] = v_rco011;
+                pv[4] = v_rco100; pv[5] = v_rco101; pv[6] = v_rco110; pv[7] = v_rco111;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // walk the valid pixels in raster order, 8 at a time: lane 8*j + k holds pixel
-            // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so one LDS float
-            // add (ds_add_f32, eight lanes) applies them, and the wave's LDS operations execute
-            // in issue order -- every bin receives its additions in exactly the serial order
+            // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so its eight
+            // lanes update them in one read-add-write, pixel after pixel
             for (int g = 0; g < nv; g += 8) {
                 const int s = g + (lane >> 3), k = lane & 7;
                 const bool act = s < nv;
@@ -1141,7 +1229,9 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
                        sb->tmp, sb->tmp_floats);
     auto blur = [&](const float* src, int64_t src_stride, float* dst, float* dog, int w, int h, int layer) {
         dim3 g((w + BT_W - 1) / BT_W, (h + BT_H - 1) / BT_H, nb);
-        hipLaunchKernelGGL(k_blur_tile, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h,
+        const int rr = ks[layer] >> 1;
+        const size_t lds = sizeof(float) * (size_t)(BT_H + 2 * rr) * (BT_W + 2 * rr + BT_W);
+        hipLaunchKernelGGL(k_blur_tile, g, dim3(256), lds, st, src, src_stride, dst, gs, dog, ds, w, h,
                            (const float*)(sb->consts + layer * KTAPS), ks[layer]);
     };
     blur(sb->tmp, sb->tmp_floats, sb->gauss + sb->gauss_off[0], nullptr, 2 * W, 2 * H, 0);
@@ -1161,9 +1251,17 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
     for (int o = 0; o < sb->n_oct; ++o) {
         const int w = sb->oct_w[o], h = sb->oct_h[o];
         if (w <= 2 * SIFT_IMG_BORDER || h <= 2 * SIFT_IMG_BORDER) continue;
-        for (int i = 1; i <= N_LAYERS; ++i)
-            hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER, nb),
-                               dim3(128), 0, st, *sb, o, i);
+        // tiled, all layers of the octave per launch (VO_SIFT_EXTREMA_ROW=1: a thread per pixel
+        // and layer, the first form; same candidate set)
+        static const int ex_row = [] { const char* e = getenv("VO_SIFT_EXTREMA_ROW"); return e ? atoi(e) : 0; }();
+        if (ex_row == 1) {
+            for (int i = 1; i <= N_LAYERS; ++i)
+                hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER, nb),
+                                   dim3(128), 0, st, *sb, o, i);
+        } else {
+            const dim3 g((w - 2 * SIFT_IMG_BORDER + EX_W - 1) / EX_W, (h - 2 * SIFT_IMG_BORDER + EX_H - 1) / EX_H, nb);
+            hipLaunchKernelGGL(k_extrema_t, g, dim3(256), 0, st, *sb, o);
+        }
     }
     const char* kser = getenv("VO_SIFT_KP_SERIAL");
     if (kser && atoi(kser) == 1) {
