@@ -154,7 +154,10 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
     const int tid = threadIdx.x;
     const int r = n >> 1;
     float* s_src = s_dyn;
-    float* s_row = s_dyn + (BT_H + 2 * r) * (BT_W + 2 * r);
+    // source row stride odd (cols + 1): the row pass's lanes read at 4-float steps from four
+    // rows, which are then spread over all LDS banks
+    const int sst = BT_W + 2 * r + 1;
+    float* s_row = s_dyn + (BT_H + 2 * r) * sst;
     const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
     src += blockIdx.z * src_stride;
     dst += blockIdx.z * dst_stride;
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
         const int lx = tid & 63, wy = tid >> 6;
         for (int ty = wy; ty < rows; ty += 4) {
             const float* srow = src + (int64_t)refl101(y0 - r + ty, h) * w;
-            for (int tx = lx; tx < cols; tx += 64) s_src[ty * cols + tx] = srow[refl101(x0 - r + tx, w)];
+            for (int tx = lx; tx < cols; tx += 64) s_src[ty * sst + tx] = srow[refl101(x0 - r + tx, w)];
         }
     }
     __syncthreads();
@@ -174,7 +177,7 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
     // output still sums its taps k = 0..n-1 in order
     for (int i = tid; i < rows * (BT_W / 4); i += 256) {
         const int ty = i >> 4, tx = (i & 15) * 4;
-        const float* sp = s_src + ty * cols + tx;
+        const float* sp = s_src + ty * sst + tx;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
         float v0 = sp[0], v1 = sp[1], v2 = sp[2];
         for (int k = 0; k < n; ++k) {
@@ -206,7 +209,7 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
                 const int gy = y0 + tyh + j;
                 if (gy >= h || gx >= w) continue;
                 dst[(int64_t)gy * w + gx] = acc[j];
-                if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc[j] - s_src[(tyh + j + r) * cols + tx + r];
+                if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc[j] - s_src[(tyh + j + r) * sst + tx + r];
             }
         }
     }
@@ -1230,7 +1233,7 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
     auto blur = [&](const float* src, int64_t src_stride, float* dst, float* dog, int w, int h, int layer) {
         dim3 g((w + BT_W - 1) / BT_W, (h + BT_H - 1) / BT_H, nb);
         const int rr = ks[layer] >> 1;
-        const size_t lds = sizeof(float) * (size_t)(BT_H + 2 * rr) * (BT_W + 2 * rr + BT_W);
+        const size_t lds = sizeof(float) * (size_t)(BT_H + 2 * rr) * (BT_W + 2 * rr + 1 + BT_W);
         hipLaunchKernelGGL(k_blur_tile, g, dim3(256), lds, st, src, src_stride, dst, gs, dog, ds, w, h,
                            (const float*)(sb->consts + layer * KTAPS), ks[layer]);
     };
