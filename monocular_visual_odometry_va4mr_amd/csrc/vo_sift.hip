@@ -878,10 +878,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
     int (*pidx_s)[64] = reinterpret_cast<int (*)[64]>(pidx_s4);
-    __shared__ float pval_s[4][64 * 8];
+    // contributions k-major with a 72-float stride: the pixel phase's stores (one per k, 64
+    // lanes) and the walk's loads (lane 8j + k reads pixel g + j's k-th) are conflict-free
+    __shared__ float pval_s[4][8 * 72];
     __shared__ float hist_s[4][384];
     __shared__ float dst_s[4][128];
     __shared__ float red_s[4][2];
+    __shared__ uint32_t ring_s[4][128];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_kp = im.counters[2];
     for (int q = blockIdx.x * 4 + w; q < n_kp; q += gridDim.x * 4) {     // wave-uniform loop
@@ -889,6 +892,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         float* pval = pval_s[w];
         float* hist = hist_s[w];
         float* dsl = dst_s[w];
+        uint32_t* ring = ring_s[w];
         const float* tab = sb.consts + EXPTAB_OFF;
         const float* kp = im.kp_out + 6 * (int64_t)q;
         const int kpo = (int)kp[5];
@@ -918,66 +922,92 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const int side = 2 * radius + 1;
         const int total = side * side;
         for (int t = lane; t < 384; t += 64) hist[t] = 0.f;
+        // Window positions in raster order, 64 at a time: the valid ones (inside the rotated
+        // descriptor square and the image) are appended, in order, to a 128-entry ring; every 64
+        // pending positions form one dense chunk whose per-pixel math runs on all 64 lanes, and
+        // whose contributions are then walked into the histogram.  Chunks stay in raster order.
+        const float inv_side = 1.f / (float)side;
+        int head = 0, pend = 0;                                      // wave-uniform ring state
         for (int base = 0; base < total; base += 64) {
             const int pos = base + lane;
-            const int ii = pos / side;
+            // pos / side from the float reciprocal: exact (pos < 2^20; margin 0.5 / side)
+            const int ii = (int)(((float)pos + 0.5f) * inv_side);
             const int i = ii - radius, j = pos - ii * side - radius;
             const float c_rot = j * cos_t - i * sin_t;
             const float r_rot = j * sin_t + i * cos_t;
-            float rbin = r_rot + d / 2 - 0.5f;
-            float cbin = c_rot + d / 2 - 0.5f;
+            const float rbin = r_rot + d / 2 - 0.5f;
+            const float cbin = c_rot + d / 2 - 0.5f;
             const int r = ptiy + i, c = ptix + j;
             const bool valid = pos < total && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 &&
                                c > 0 && c < cols - 1;
-            // compaction slot first, so each contribution goes to LDS as soon as it is formed
             const uint64_t m = __ballot(valid);
-            const int nv = __popcll(m);
-            if (valid) {
-                const int slot = __popcll(m & ((1ull << lane) - 1ull));
-                float* pv = pval + slot * 8;
-                const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
-                const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
-                const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
-                const float o = fast_atan2(dy, dx);
-                const float mag = sqrtf(dx * dx + dy * dy) * wgt;
-                float obin = (o - ori) * bins_per_rad;
-                int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
-                rbin -= r0; cbin -= c0; obin -= o0;
-                if (o0 < 0) o0 += n;
-                if (o0 >= n) o0 -= n;
-                pidx[slot] = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-                // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
-                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                pv[0] = v_rco000; pv[1] = v_rco001; pv[2] = v_rco010; pv[3] = v_rco011;
-                pv[4] = v_rco100; pv[5] = v_rco101; pv[6] = v_rco110; pv[7] = v_rco111;
-            }
+            if (valid)
+                ring[(head + pend + __popcll(m & ((1ull << lane) - 1ull))) & 127] =
+                    (uint32_t)(uint16_t)i | ((uint32_t)(uint16_t)j << 16);
+            pend += __popcll(m);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // walk the valid pixels in raster order, 8 at a time: lane 8*j + k holds pixel
-            // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so its eight
-            // lanes update them in one read-add-write, pixel after pixel
-            for (int g = 0; g < nv; g += 8) {
-                const int s = g + (lane >> 3), k = lane & 7;
-                const bool act = s < nv;
-                const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
-                const int addr = act ? pidx[s] + koff : 0;
-                const float v = act ? pval[g * 8 + lane] : 0.f;
-                // pixel j's eight lanes read their bins, add, write back; the next pixel's
-                // read is issued after this write (a wave's LDS operations execute in order)
-                const uint64_t am = __ballot(act);
-    #pragma unroll
-                for (int j = 0; j < 8; ++j) lds_rmw_add_lanes(hist + addr, v, am & (0xFFull << (8 * j)));
+            const bool last = base + 64 >= total;
+            while (pend >= 64 || (last && pend > 0)) {
+                const int take = pend < 64 ? pend : 64;
+                if (lane < take) {
+                    const uint32_t e = ring[(head + lane) & 127];
+                    const int pi = (int)(int16_t)(e & 0xFFFF), pj = (int)(int16_t)(e >> 16);
+                    // the same operations as the validity test above
+                    const float pc_rot = pj * cos_t - pi * sin_t;
+                    const float pr_rot = pj * sin_t + pi * cos_t;
+                    float rb = pr_rot + d / 2 - 0.5f;
+                    float cb = pc_rot + d / 2 - 0.5f;
+                    const int pr = ptiy + pi, pc = ptix + pj;
+                    const float dx = DAT(img, cols, pr, pc + 1) - DAT(img, cols, pr, pc - 1);
+                    const float dy = DAT(img, cols, pr - 1, pc) - DAT(img, cols, pr + 1, pc);
+                    const float wgt = exp32f((pc_rot * pc_rot + pr_rot * pr_rot) * exp_scale, tab);
+                    const float o = fast_atan2(dy, dx);
+                    const float mag = sqrtf(dx * dx + dy * dy) * wgt;
+                    float obin = (o - ori) * bins_per_rad;
+                    int r0 = (int)floorf(rb), c0 = (int)floorf(cb), o0 = (int)floorf(obin);
+                    rb -= r0; cb -= c0; obin -= o0;
+                    if (o0 < 0) o0 += n;
+                    if (o0 >= n) o0 -= n;
+                    pidx[lane] = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+                    // slot order = bin offset order {0, 1, 10, 11, 60, 61, 70, 71}
+                    const float v_r1 = mag * rb, v_r0 = mag - v_r1;
+                    const float v_rc11 = v_r1 * cb, v_rc10 = v_r1 - v_rc11;
+                    const float v_rc01 = v_r0 * cb, v_rc00 = v_r0 - v_rc01;
+                    const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                    const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                    const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                    const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                    pval[0 * 72 + lane] = v_rco000; pval[1 * 72 + lane] = v_rco001;
+                    pval[2 * 72 + lane] = v_rco010; pval[3 * 72 + lane] = v_rco011;
+                    pval[4 * 72 + lane] = v_rco100; pval[5 * 72 + lane] = v_rco101;
+                    pval[6 * 72 + lane] = v_rco110; pval[7 * 72 + lane] = v_rco111;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // walk the valid pixels in raster order, 8 at a time: lane 8*j + k holds pixel
+                // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so its eight
+                // lanes update them in one read-add-write, pixel after pixel
+                for (int g = 0; g < take; g += 8) {
+                    const int s = g + (lane >> 3), k = lane & 7;
+                    const bool act = s < take;
+                    const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
+                    const int addr = act ? pidx[s] + koff : 0;
+                    const float v = act ? pval[k * 72 + s] : 0.f;
+                    // pixel j's eight lanes read their bins, add, write back; the next pixel's
+                    // read is issued after this write (a wave's LDS operations execute in order)
+                    const uint64_t am = __ballot(act);
+        #pragma unroll
+                    for (int j = 0; j < 8; ++j) lds_rmw_add_lanes(hist + addr, v, am & (0xFFull << (8 * j)));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                head = (head + take) & 127;
+                pend -= take;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         // circular orientation wrap + copy (independent per output)
         for (int t = lane; t < d * d * n; t += 64) {
