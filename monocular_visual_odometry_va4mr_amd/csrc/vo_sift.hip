@@ -873,6 +873,22 @@ VO_DEV void lds_rmw_add_lanes(float* p, float v, uint64_t lanes)
                  : "memory");
 }
 
+// The same for a run of up to four pixels with the same eight bins: one read, the four adds in
+// pixel order (missing pixels add +0, which leaves a bin unchanged: every contribution and
+// every partial sum is >= +0), one write.
+VO_DEV void lds_rmw_add4_lanes(float* p, float v0, float v1, float v2, float v3, uint64_t lanes)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
+    uint64_t save;
+    float h;
+    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %7\n\tds_read_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\t"
+                 "v_add_f32 %1, %1, %3\n\tv_add_f32 %1, %1, %4\n\tv_add_f32 %1, %1, %5\n\tv_add_f32 %1, %1, %6\n\t"
+                 "ds_write_b32 %2, %1\n\ts_mov_b64 exec, %0"
+                 : "=&s"(save), "=&v"(h)
+                 : "v"(a), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(lanes)
+                 : "memory");
+}
+
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_sift_desc_w(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
@@ -885,6 +901,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     __shared__ float dst_s[4][128];
     __shared__ float red_s[4][2];
     __shared__ uint32_t ring_s[4][128];
+    __shared__ int slist_s[4][64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_kp = im.counters[2];
     for (int q = blockIdx.x * 4 + w; q < n_kp; q += gridDim.x * 4) {     // wave-uniform loop
@@ -893,6 +910,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         float* hist = hist_s[w];
         float* dsl = dst_s[w];
         uint32_t* ring = ring_s[w];
+        int* slist = slist_s[w];
         const float* tab = sb.consts + EXPTAB_OFF;
         const float* kp = im.kp_out + 6 * (int64_t)q;
         const int kpo = (int)kp[5];
@@ -987,20 +1005,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                // walk the valid pixels in raster order, 8 at a time: lane 8*j + k holds pixel
-                // (g + j)'s k-th contribution; pixel j's eight bins are distinct, so its eight
-                // lanes update them in one read-add-write, pixel after pixel
-                for (int g = 0; g < take; g += 8) {
-                    const int s = g + (lane >> 3), k = lane & 7;
-                    const bool act = s < take;
-                    const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
-                    const int addr = act ? pidx[s] + koff : 0;
-                    const float v = act ? pval[k * 72 + s] : 0.f;
-                    // pixel j's eight lanes read their bins, add, write back; the next pixel's
-                    // read is issued after this write (a wave's LDS operations execute in order)
-                    const uint64_t am = __ballot(act);
+                // walk the chunk's pixels in raster order.  Consecutive pixels with the same base
+                // bin (common: the smoothed gradient changes slowly) form runs, cut into sub-runs
+                // of at most four; a sub-run is one read-add-write of its eight bins by eight
+                // lanes (lds_rmw_add4_lanes), sub-runs one after another, 8 per group: lane
+                // 8*j + k serves sub-run g + j, bin offset k.  Each bin still receives its
+                // additions one at a time in pixel order.
+                {
+                    const int my_idx = lane < take ? pidx[lane] : -1;
+                    const int prv = __shfl_up(my_idx, 1, 64);
+                    const uint64_t rs = __ballot(lane < take && (lane == 0 || my_idx != prv));   // run starts
+                    const uint64_t upto = rs & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+                    const int last = 63 - __clzll((long long)upto);                             // this run's start
+                    const uint64_t ss = __ballot(lane < take && ((lane - last) & 3) == 0);       // sub-run starts
+                    if ((ss >> lane) & 1ull) slist[__popcll(ss & ((1ull << lane) - 1ull))] = lane;
+                    const int ns = __popcll(ss);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (int g = 0; g < ns; g += 8) {
+                        const int rr = g + (lane >> 3), k = lane & 7;
+                        const bool act = rr < ns;
+                        const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
+                        const int s0 = act ? slist[rr] : 0;
+                        const int e0 = act ? (rr + 1 < ns ? slist[rr + 1] : take) : 0;
+                        const int m = e0 - s0;                                           // 1..4
+                        const int addr = act ? pidx[s0] + koff : 0;
+                        const float* pv = pval + k * 72 + s0;
+                        const float v0 = act ? pv[0] : 0.f;
+                        const float v1 = act && m > 1 ? pv[1] : 0.f;
+                        const float v2 = act && m > 2 ? pv[2] : 0.f;
+                        const float v3 = act && m > 3 ? pv[3] : 0.f;
+                        const uint64_t am = __ballot(act);
         #pragma unroll
-                    for (int j = 0; j < 8; ++j) lds_rmw_add_lanes(hist + addr, v, am & (0xFFull << (8 * j)));
+                        for (int j = 0; j < 8; ++j)
+                            lds_rmw_add4_lanes(hist + addr, v0, v1, v2, v3, am & (0xFFull << (8 * j)));
+                    }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
