@@ -156,6 +156,11 @@ int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t st
 int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force,
                    vo_stream_t stream);
 
+/* vo_pnp followed by vo_triangulate(force = 0) as one launch, each chain's triangulation in the
+ * block that solved its pose (the engine's step; same results as the two calls).  No reference
+ * counterpart of its own: it replaces the pair VisualOdometryPipeLine.py:342-358 + :366-368. */
+int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
+
 /* cv2.goodFeaturesToTrack (:256) on pyramid level 0 of pyr[cur] -> state->corners. */
 int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream);
 

@@ -1616,7 +1616,7 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
 }
 
 // ---------------------------------------------------------------- GFTT selection
-#define SEL_THREADS 1024
+#define SEL_THREADS 512
 #define PAGE 4096
 #define ACC_MAX 8192
 #define GRID_LDS_CELLS 22528
@@ -1666,7 +1666,8 @@ __device__ long long g_selprof[16];
 #define SELPROF(i) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(SEL_THREADS) k_gftt_select(SelParams P)
+template <int NT>
+__global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
 {
     // dynamic LDS sized by the host (vo_gftt): page | accepted xy | grid (if it fits)
     extern __shared__ uint64_t sel_dyn[];
@@ -2297,11 +2298,21 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
         static const int noglb = [] { const char* e = getenv("VO_SEL_SERIAL_L2"); return e ? atoi(e) : 0; }();
         S.grid_glb = !noglb && S.grid_lds == 0 && SEL_GG_OFF + 2 * cells <= S.gstride;
         const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
-        static const bool attr_ok = hipFuncSetAttribute((const void*)k_gftt_select,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        150 * 1024) == hipSuccess;
+        static const bool attr_ok =
+            hipFuncSetAttribute((const void*)k_gftt_select<SEL_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                150 * 1024) == hipSuccess &&
+            hipFuncSetAttribute((const void*)k_gftt_select<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) ==
+                hipSuccess &&
+            hipFuncSetAttribute((const void*)k_gftt_select<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024) ==
+                hipSuccess;
         if (!attr_ok && lds > 64 * 1024) return VO_EHIP;
-        hipLaunchKernelGGL(k_gftt_select, dim3(d->B), dim3(SEL_THREADS), lds, st, S);
+        // block size SEL_THREADS = 512, or VO_SEL_THREADS = 256 / 1024 (same result).  Headline
+        // bench: 512 threads 56.2k frames/s, 1024 55.1k, 256 55.9k -- a select block holds its
+        // wave slots while the other stream group's LK runs
+        static const int nt_env = [] { const char* e = getenv("VO_SEL_THREADS"); return e ? atoi(e) : SEL_THREADS; }();
+        if (nt_env == 256) hipLaunchKernelGGL(k_gftt_select<256>, dim3(d->B), dim3(256), lds, st, S);
+        else if (nt_env == 1024) hipLaunchKernelGGL(k_gftt_select<1024>, dim3(d->B), dim3(1024), lds, st, S);
+        else hipLaunchKernelGGL(k_gftt_select<SEL_THREADS>, dim3(d->B), dim3(SEL_THREADS), lds, st, S);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
 }

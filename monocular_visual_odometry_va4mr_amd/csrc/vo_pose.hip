@@ -432,7 +432,7 @@ struct PnPArgs {
     int32_t* n_inl;         // [B]
 };
 
-__global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
+VO_DEV void pnp_ransac_block(const PnPArgs& A)
 {
     __shared__ int sub[HYP][4];
     __shared__ double mdl[HYP][12];
@@ -606,8 +606,8 @@ __global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A)
 }
 
 // engine epilogue of the PnP step (:342-358): guard, inlier filtering, Rodrigues, inversion
-__global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const double* rvec, const double* tvec,
-                                                   const int32_t* success, const uint8_t* mask_all)
+VO_DEV void pnp_apply_block(const vo_dims& d, const vo_state& s, const double* rvec, const double* tvec,
+                            const int32_t* success, const uint8_t* mask_all)
 {
     __shared__ int lds[16];
     __shared__ double Rwc[9];
@@ -662,6 +662,32 @@ __global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const 
         for (int i = 0; i < 3; ++i)
             tcw[i] = __builtin_fma(-Rcw[i * 3 + 2], t[2], __builtin_fma(-Rcw[i * 3 + 1], t[1], -Rcw[i * 3] * t[0]));
     }
+}
+
+__global__ void __launch_bounds__(256) k_pnp_ransac(PnPArgs A) { pnp_ransac_block(A); }
+
+__global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const double* rvec, const double* tvec,
+                                                   const int32_t* success, const uint8_t* mask_all)
+{
+    pnp_apply_block(d, s, rvec, tvec, success, mask_all);
+}
+
+// the engine's PnP stage as one launch: RANSAC + EPnP, then (after a block barrier, which
+// makes thread 0's rvec / tvec / success visible to the block) the epilogue -- a second,
+// separate launch had to wait for CUs behind the other stream group's LK blocks
+// At most 256 registers per lane (VGPR + AGPR) -- two waves per SIMD, some spilled to scratch --
+// so that two chains' blocks fit on one CU: with 384 chains per launch on 256 CUs, a block
+// needing a whole CU left a third of the chains to start only after the other stream group's LK
+// flood (which refills every freed wave slot) had drained.
+#ifndef VO_PNP_WPE
+#define VO_PNP_WPE 2
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VO_PNP_WPE, 8)))
+k_pnp_fused(PnPArgs A, vo_dims d, vo_state s)
+{
+    pnp_ransac_block(A);
+    __syncthreads();
+    pnp_apply_block(d, s, A.rvec, A.tvec, A.success, A.mask);
 }
 
 // ------------------------------------------------------------------ triangulation
@@ -722,7 +748,7 @@ struct TriArgs {
     int force;
 };
 
-__global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
+VO_DEV void triangulate_block(const TriArgs& A)
 {
     __shared__ int lds[16];
     __shared__ double Rc[9], tc[3], Rcwc[9], tcwc[3], Pc[12];
@@ -827,6 +853,20 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A)
         s.nC[b] = kept;
         if (sh_fail) s.status[b] = VO_ST_CAPACITY;
     }
+}
+
+__global__ void __launch_bounds__(256) k_triangulate(TriArgs A) { triangulate_block(A); }
+
+// vo_pnp + vo_triangulate(force 0) as one launch (the engine's step): the triangulation of a
+// chain runs in the block that just solved its pose, instead of waiting for CUs again
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VO_PNP_WPE, 8)))
+k_pnp_tri(PnPArgs A, TriArgs T)
+{
+    pnp_ransac_block(A);
+    __syncthreads();
+    pnp_apply_block(T.d, T.s, A.rvec, A.tvec, A.success, A.mask);
+    __syncthreads();
+    triangulate_block(T);
 }
 
 // ------------------------------------------------ feature adding + step finish
@@ -999,27 +1039,35 @@ extern "C" int vo_pnp_ransac(const vo_opts* o, int B, const float* obj, const fl
     return hip_rc();
 }
 
-extern "C" int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+static void fill_pnp_engine(PnPArgs& P, const vo_dims* d, const vo_opts* o, const vo_state* s)
 {
-    if (!d || !o || !s) return VO_EARG;
-    if (d->work_stride < 12LL * d->ncap + 64) return VO_EARG;
-    PnPArgs P;
     fill_pnp(P, o);
     P.min_points = 8;                                                   // :342
     P.obj = s->lm_X; P.img = s->lm_kp; P.counts = s->nL; P.cap = d->ncap; P.chain_status = s->status;
     P.work = s->work; P.work_stride = d->work_stride; P.iwork = s->iwork; P.iwork_stride = d->iwork_stride;
     P.rvec = s->pnp_rt; P.tvec = s->pnp_rt + 3LL * d->B;
     P.success = s->pnp_ok; P.n_inl = s->pnp_ninl; P.mask = s->pnp_mask;
+}
+
+extern "C" int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    if (d->work_stride < 12LL * d->ncap + 64) return VO_EARG;
+    PnPArgs P;
+    fill_pnp_engine(P, d, o, s);
     hipStream_t st = VO_STREAM(stream);
-    hipLaunchKernelGGL(k_pnp_ransac, dim3(d->B), dim3(256), 0, st, P);
-    hipLaunchKernelGGL(k_pnp_apply, dim3(d->B), dim3(256), 0, st, *d, *s, P.rvec, P.tvec, P.success, P.mask);
+    static const int split = [] { const char* e = getenv("VO_PNP_SPLIT"); return e ? atoi(e) : 0; }();
+    if (split == 1) {                     // the two-launch form (A/B measurements)
+        hipLaunchKernelGGL(k_pnp_ransac, dim3(d->B), dim3(256), 0, st, P);
+        hipLaunchKernelGGL(k_pnp_apply, dim3(d->B), dim3(256), 0, st, *d, *s, P.rvec, P.tvec, P.success, P.mask);
+    } else {
+        hipLaunchKernelGGL(k_pnp_fused, dim3(d->B), dim3(256), 0, st, P, *d, *s);
+    }
     return hip_rc();
 }
 
-extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force, vo_stream_t stream)
+static void fill_tri(TriArgs& A, const vo_dims* d, const vo_opts* o, const vo_state* s, int force)
 {
-    if (!d || !o || !s) return VO_EARG;
-    TriArgs A;
     A.d = *d;
     A.s = *s;
     for (int i = 0; i < 9; ++i) { A.K[i] = o->K[i]; A.Kinv[i] = o->K_inv[i]; }
@@ -1028,7 +1076,26 @@ extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state
     A.cos_thr = o->cos_baseline;
     A.min_frames = o->min_baseline_frames;
     A.force = force;
+}
+
+extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    TriArgs A;
+    fill_tri(A, d, o, s, force);
     hipLaunchKernelGGL(k_triangulate, dim3(d->B), dim3(256), 0, VO_STREAM(stream), A);
+    return hip_rc();
+}
+
+extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    if (!d || !o || !s) return VO_EARG;
+    if (d->work_stride < 12LL * d->ncap + 64) return VO_EARG;
+    PnPArgs P;
+    fill_pnp_engine(P, d, o, s);
+    TriArgs T;
+    fill_tri(T, d, o, s, 0);
+    hipLaunchKernelGGL(k_pnp_tri, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     return hip_rc();
 }
 

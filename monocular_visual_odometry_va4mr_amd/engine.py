@@ -275,8 +275,13 @@ class Engine:
             main.wait_stream(bulk)
         else:
             run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
-        run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
-        run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
+        if getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1"):
+            # one launch for both stages (vo_pnp_triangulate); stage 3 is then empty
+            run(2, main, lambda: lib.vo_pnp_triangulate(pd, po, ps, sm))
+            run(3, main, lambda: 0)
+        else:
+            run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
+            run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
         if forked:
             main.wait_stream(side)                                # corners ready
         run(5, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))

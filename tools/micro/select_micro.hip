@@ -29,7 +29,7 @@ int main()
     S.gscratch = dgrid; S.gstride = (int64_t)W * H; S.chain_status = dst;
     S.acc_lds = mcap; S.grid_lds = ((W + 9) / 10) * ((H + 9) / 10);
     const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
-    CK(hipFuncSetAttribute((const void*)k_gftt_select, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+    CK(hipFuncSetAttribute((const void*)k_gftt_select<SEL_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     std::vector<float> ref(2 * 1400);
     {
@@ -43,7 +43,7 @@ int main()
         CK(hipMemset(dst, 0, 4));
         { long long z[16] = {0}; CK(hipMemcpyToSymbol(HIP_SYMBOL(g_selprof), z, sizeof z)); }
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k_gftt_select, dim3(1), dim3(SEL_THREADS), lds, 0, S);
+        hipLaunchKernelGGL(k_gftt_select<SEL_THREADS>, dim3(1), dim3(SEL_THREADS), lds, 0, S);
         CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
         float ms; CK(hipEventElapsedTime(&ms, e0, e1));
         long long t[16];
