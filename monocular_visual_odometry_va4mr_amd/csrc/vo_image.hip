@@ -906,11 +906,15 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
                     const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
                     const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int b1 = 0, b2 = 0;
+                    // all four quads read before the (wave-uniform) branch: one LDS round trip
+                    uint32_t qv[MAXJ];
+#pragma unroll
+                    for (int j = 0; j < MAXJ; ++j) qv[j] = tb[toff[j]];
                     // the iw11 = -1 correction only in its own (wave-uniform) copy of the loop
                     auto mismatch = [&](auto negc) {
 #pragma unroll
                         for (int j = 0; j < MAXJ; ++j) {
-                            const uint32_t q = tb[toff[j]];
+                            const uint32_t q = qv[j];
                             uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
                                            __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                             if (decltype(negc)::value) sum -= q >> 24;
@@ -1577,8 +1581,18 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
         eA = eB;
         eB = v;
     };
-    for (int ir = g0 - 1; ir <= g1 + 1; ++ir) {
-        const int iv = colp[(int64_t)ir * P.pitch];
+    // image rows are loaded E3_PF rows ahead of their use (a register ring), so the row loop
+    // does not wait a full memory round trip per row
+    constexpr int E3_PF = 8;
+    int pf[E3_PF];
+    const int ir_end = g1 + 1;
+#pragma unroll
+    for (int k = 0; k < E3_PF; ++k) pf[k] = (g0 - 1 + k <= ir_end) ? colp[(int64_t)(g0 - 1 + k) * P.pitch] : 0;
+    for (int ir = g0 - 1; ir <= ir_end; ++ir) {
+        const int iv = pf[0];
+#pragma unroll
+        for (int k = 0; k < E3_PF - 1; ++k) pf[k] = pf[k + 1];
+        pf[E3_PF - 1] = (ir + E3_PF <= ir_end) ? colp[(int64_t)(ir + E3_PF) * P.pitch] : 0;
         const int il = dpp_from_left(iv), irt = dpp_from_right(iv);
         const int hs = il + 2 * iv + irt, hd = irt - il;
         if (ir >= g0 + 1) {
