@@ -92,9 +92,8 @@ class VisualOdometryPipeLine:
         else:
             eng.step(img[None])
         self._frame = img
-        st = self._status()
+        st, n_inl = eng.status_word()                          # one host sync per frame
         if st == L.ST_OK:
-            n_inl = int(eng.t["nInl"][0])
             if len(self.num_tracked_landmarks_list) == 20:     # :360-364
                 self.num_tracked_landmarks_list.pop(0)
             self.num_tracked_landmarks_list.append(n_inl)

@@ -859,7 +859,8 @@ __global__ void __launch_bounds__(256) k_triangulate(TriArgs A) { triangulate_bl
 
 // vo_pnp + vo_triangulate(force 0) as one launch (the engine's step): the triangulation of a
 // chain runs in the block that just solved its pose, instead of waiting for CUs again
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VO_PNP_WPE, 8)))
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 k_pnp_tri(PnPArgs A, TriArgs T)
 {
     pnp_ransac_block(A);
@@ -1095,7 +1096,16 @@ extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_s
     fill_pnp_engine(P, d, o, s);
     TriArgs T;
     fill_tri(T, d, o, s, 0);
-    hipLaunchKernelGGL(k_pnp_tri, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
+    // more chains than CUs: the 2-waves/SIMD build (two blocks per CU, some registers spilled);
+    // otherwise every block has a CU of its own and the unconstrained build is faster
+    static const int n_cu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return n;
+    }();
+    if (d->B > n_cu) hipLaunchKernelGGL(k_pnp_tri<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
+    else hipLaunchKernelGGL(k_pnp_tri<1>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     return hip_rc();
 }
 

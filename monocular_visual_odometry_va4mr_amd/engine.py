@@ -201,6 +201,18 @@ class Engine:
     def statuses(self) -> np.ndarray:
         return self.t["status"].cpu().numpy()
 
+    def status_word(self) -> tuple[int, int]:
+        """(status, inlier count) of chain 0 with one host synchronisation: both gathered on
+        the device, one copy into a pinned host word (the drop-in class reads them after
+        every frame)."""
+        if getattr(self, "_sw_host", None) is None:
+            self._sw_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
+            self._sw_host = torch.zeros(2, dtype=torch.int32).pin_memory()
+        torch.cat([self.t["status"][:1], self.t["nInl"][:1]], out=self._sw_dev)
+        self._sw_host.copy_(self._sw_dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return int(self._sw_host[0]), int(self._sw_host[1])
+
     # ------------------------------------------------------------------ stages
     def build_pyramid(self, frames: torch.Tensor, which: int, deriv: bool = False):
         """Pyramid + Scharr derivatives of `frames` into pyr[which] / der[which] (vo_pyr_build
