@@ -164,12 +164,31 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
     if (tid < n) s_k[tid] = kern[tid];
     const int rows = BT_H + 2 * r, cols = BT_W + 2 * r;
     // staging: 64 lanes along a row, the four waves on rows w, w+4, ... (reflection computed per
-    // row / column, no division per element)
+    // row / column, no division per element).  Fixed trip counts, unrolled: every load of the
+    // tile is in flight before the first LDS store (a load-store loop waited one memory round
+    // trip per trip)
     {
+        constexpr int NR = (BT_H + 2 * BT_R + 3) / 4, NC = (BT_W + 2 * BT_R + 63) / 64;
         const int lx = tid & 63, wy = tid >> 6;
-        for (int ty = wy; ty < rows; ty += 4) {
+        int xo[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) xo[c] = refl101(x0 - r + min(lx + 64 * c, cols - 1), w);
+        float v[NR][NC];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int ty = min(wy + 4 * j, rows - 1);
             const float* srow = src + (int64_t)refl101(y0 - r + ty, h) * w;
-            for (int tx = lx; tx < cols; tx += 64) s_src[ty * sst + tx] = srow[refl101(x0 - r + tx, w)];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[j][c] = srow[xo[c]];
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int ty = wy + 4 * j;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int tx = lx + 64 * c;
+                if (ty < rows && tx < cols) s_src[ty * sst + tx] = v[j][c];
+            }
         }
     }
     __syncthreads();
@@ -273,68 +292,115 @@ __global__ void k_extrema(vo_sift_buf sb, int o, int layer)
 
 // All three extremum layers of one octave from one LDS tile: 64 x 16 interior pixels per
 // block, the five DoG layers of the octave with a 1-pixel halo staged once; each pixel that
-// passes the threshold is compared with the max / min of its 3x3x3 neighbourhood (all 27 reads
-// independent, no early exit -- the per-pixel loop with an exit at the first failing neighbour
-// was a chain of dependent global loads).  The test is findScaleSpaceExtrema's:
+// passes the threshold is compared with the max / min of its 3x3x3 neighbourhood (separable:
+// 3-wide row max / min per layer and row, then 3 rows x 3 layers; no early exit -- the
+// per-pixel loop with an exit at the first failing neighbour was a chain of dependent global
+// loads).  The test is findScaleSpaceExtrema's:
 // val > 0 && val >= every neighbour, or val < 0 && val <= every neighbour (the centre itself is
 // one of the 27, which changes nothing).  Candidates are appended with one atomic per wave; the
 // list order is irrelevant (keypoints are sorted canonically).
 #define EX_W 64
 #define EX_H 16
+#define EX_LCAP 1024                      // candidates per block held in LDS (more: flagged)
 __global__ void __launch_bounds__(256) k_extrema_t(vo_sift_buf sb, int o)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ float t[N_LAYERS + 2][EX_H + 2][EX_W + 2];
+    __shared__ int2 s_list[EX_LCAP];
+    __shared__ int s_n, s_base;
     const int w = sb.oct_w[o], h = sb.oct_h[o];
     const int x0 = SIFT_IMG_BORDER + blockIdx.x * EX_W, y0 = SIFT_IMG_BORDER + blockIdx.y * EX_H;
     const int tid = threadIdx.x;
+    if (tid == 0) s_n = 0;
     const float* dog0 = im.dog + sb.dog_off[o * (N_LAYERS + 2)];
     const int64_t plane = (int64_t)w * h;               // the octave's DoG layers are contiguous
-    for (int i = tid; i < (N_LAYERS + 2) * (EX_H + 2) * (EX_W + 2); i += 256) {
+    // every load of the tile in flight before the first LDS store (fixed, unrolled trip count;
+    // clamped addresses, zeros written outside the octave)
+    constexpr int NT = (N_LAYERS + 2) * (EX_H + 2) * (EX_W + 2), NL = (NT + 255) / 256;
+    const __amdgpu_buffer_rsrc_t rdog =
+        __builtin_amdgcn_make_buffer_rsrc((void*)dog0, (short)0, (int)(4 * (N_LAYERS + 2) * plane), 0x00020000);
+    float v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = min(tid + 256 * k, NT - 1);
         const int l = i / ((EX_H + 2) * (EX_W + 2));
         const int rem = i - l * (EX_H + 2) * (EX_W + 2);
         const int ty = rem / (EX_W + 2), tx = rem - ty * (EX_W + 2);
-        const int gy = y0 - 1 + ty, gx = x0 - 1 + tx;
-        t[l][ty][tx] = (gy < h && gx < w) ? dog0[l * plane + (int64_t)gy * w + gx] : 0.f;
+        const int gy = min(y0 - 1 + ty, h - 1), gx = min(x0 - 1 + tx, w - 1);
+        // buffer loads: 32-bit offsets, one VGPR per load
+        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdog, 4 * (l * (int)plane + gy * w + gx), 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int i = tid + 256 * k;
+        if (i < NT) {
+            const int l = i / ((EX_H + 2) * (EX_W + 2));
+            const int rem = i - l * (EX_H + 2) * (EX_W + 2);
+            const int ty = rem / (EX_W + 2), tx = rem - ty * (EX_W + 2);
+            t[l][ty][tx] = (y0 - 1 + ty < h && x0 - 1 + tx < w) ? v[k] : 0.f;
+        }
     }
     __syncthreads();
     const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
     const int tx = tid & (EX_W - 1), ty0 = (tid >> 6) * (EX_H / 4);
     const int c = x0 + tx;
     const int lane = tid & 63;
-    for (int layer = 1; layer <= N_LAYERS; ++layer) {
+    // a thread's four pixels are one column, rows ty0..ty0+3: the 3-wide row max / min of the six
+    // tile rows under them, for all five layers, is read once (18 LDS reads per layer) and each
+    // pixel's 27-neighbourhood max / min is the max / min of 9 of these
+    constexpr int R = EX_H / 4 + 2;
+    float hx[N_LAYERS + 2][R], hn[N_LAYERS + 2][R], ctr[N_LAYERS + 2][EX_H / 4];
+    // layer l's row max / min are formed right before they are first needed (layer l - 1's
+    // pixels), so at most three layers of them are live (fully unrolled)
+#pragma unroll
+    for (int l = 0; l < N_LAYERS + 2; ++l) {
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+            const float a0 = t[l][ty0 + rr][tx], a1 = t[l][ty0 + rr][tx + 1], a2 = t[l][ty0 + rr][tx + 2];
+            hx[l][rr] = fmaxf(fmaxf(a0, a1), a2);
+            hn[l][rr] = fminf(fminf(a0, a1), a2);
+            if (rr >= 1 && rr <= EX_H / 4) ctr[l][rr - 1] = a1;
+        }
+        const int layer = l - 1;
+        if (layer < 1) continue;
+#pragma unroll
         for (int k = 0; k < EX_H / 4; ++k) {
-            const int ty = ty0 + k, r = y0 + ty;
-            const float val = t[layer][ty + 1][tx + 1];
+            const int r = y0 + ty0 + k;
+            const float val = ctr[layer][k];
             bool ext = c < w - SIFT_IMG_BORDER && r < h - SIFT_IMG_BORDER && fabsf(val) > threshold;
-            if (ext) {
-                float mx = val, mn = val;
-    #pragma unroll
-                for (int dz = -1; dz <= 1; ++dz)
-    #pragma unroll
-                    for (int dy = 0; dy < 3; ++dy)
-    #pragma unroll
-                        for (int dx = 0; dx < 3; ++dx) {
-                            const float u = t[layer + dz][ty + dy][tx + dx];
-                            mx = fmaxf(mx, u);
-                            mn = fminf(mn, u);
-                        }
-                ext = val > 0 ? val >= mx : val <= mn;
-            }
+            float mx = val, mn = val;
+#pragma unroll
+            for (int dz = -1; dz <= 1; ++dz)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    mx = fmaxf(mx, hx[layer + dz][k + dy]);
+                    mn = fminf(mn, hn[layer + dz][k + dy]);
+                }
+            ext = ext && (val > 0 ? val >= mx : val <= mn);
             const uint64_t m = __ballot(ext);
             if (m == 0) continue;
+            // block-local list first (LDS atomic per wave): one global atomic per block at the
+            // end -- a global atomic per wave on the image's one counter serialised in L2
             const int leader = __ffsll((unsigned long long)m) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(&im.counters[0], __popcll(m));
+            if (lane == leader) base = atomicAdd(&s_n, __popcll(m));
             base = __shfl(base, leader, 64);
             if (!ext) continue;
             const int q = base + __popcll(m & ((1ull << lane) - 1ull));
-            if (q < sb.cand_cap) {
-                im.cand[4 * q] = o; im.cand[4 * q + 1] = layer; im.cand[4 * q + 2] = r; im.cand[4 * q + 3] = c;
-            } else {
-                im.counters[3] = 1;
-            }
+            if (q < EX_LCAP) s_list[q] = make_int2(layer, (r << 16) | c);
         }
+    }
+    __syncthreads();
+    const int nl = s_n;
+    if (nl == 0) return;
+    if (tid == 0) s_base = atomicAdd(&im.counters[0], nl);
+    __syncthreads();
+    const int gbase = s_base;
+    for (int i = tid; i < nl; i += 256) {
+        const int q = gbase + i;
+        if (i >= EX_LCAP || q >= sb.cand_cap) { im.counters[3] = 1; continue; }   // capacity: flagged
+        const int2 e = s_list[i];
+        im.cand[4 * q] = o; im.cand[4 * q + 1] = e.x; im.cand[4 * q + 2] = e.y >> 16; im.cand[4 * q + 3] = e.y & 0xFFFF;
     }
 }
 
