@@ -1675,6 +1675,14 @@ VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
 
 #ifdef VO_SELECT_PROF
 __device__ long long g_selprof[16];
+}  // namespace
+// diagnostics build only (libvo_hip_selprof.so, tools/sel_prof.py): block 0's phase timestamps
+// of the last k_gftt_select launch (100 MHz wall clock)
+extern "C" int vo_select_prof_read(long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_selprof), sizeof(long long) * 16) == hipSuccess ? 0 : -2;
+}
+namespace {
 #define SELPROF(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_selprof[i] = wall_clock64(); } while (0)
 #else
 #define SELPROF(i) do { } while (0)
@@ -1683,13 +1691,17 @@ __device__ long long g_selprof[16];
 template <int NT>
 __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
 {
-    // dynamic LDS sized by the host (vo_gftt): page | accepted xy | grid (if it fits)
+    // dynamic LDS sized by the host (vo_gftt): page | candidate xy | accepted xy | grid + cell
+    // heads (if they fit) | two conflict slots per candidate
     extern __shared__ uint64_t sel_dyn[];
     uint64_t* page = sel_dyn;
     uint32_t* cand_xy = (uint32_t*)(sel_dyn + PAGE);
     uint32_t* acc_xy = cand_xy + PAGE;
     uint32_t* lgrid = acc_xy + P.acc_lds;
     int* head = (int*)(lgrid + P.grid_lds);
+    // each candidate's first two earlier conflicts, in LDS (most have at most two); the rest of
+    // its list (up to CONF_K) is in the per-chain global scratch
+    uint16_t* cf2 = (uint16_t*)(head + P.grid_lds);
     __shared__ uint32_t round_xy[64];
     __shared__ int hist[256];
     __shared__ int sh_int[16];
@@ -1709,13 +1721,23 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
     const float thr = (float)((double)fkey_inv(P.eig_max[b]) * P.quality);
     const uint64_t lo = ((uint64_t)fkey(thr) + 1ull) << 32;
     int nk = 0;
-    for (int base = 0; base < nk_all; base += blockDim.x) {
-        const int i = base + tid;
-        const uint64_t kk = i < nk_all ? keys[i] : 0ull;
-        const bool ok = i < nk_all && kk >= lo;
+    // eight consecutive keys per thread per pass (one block scan per 8 * NT keys); every key of
+    // a pass is read before the scan's barrier, and writes never pass a later pass's reads
+    constexpr int KPT = 8;
+    for (int base = 0; base < nk_all; base += NT * KPT) {
+        const int i0 = base + tid * KPT;
+        uint64_t kk[KPT];
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            kk[j] = i0 + j < nk_all ? keys[i0 + j] : 0ull;
+            cnt += (i0 + j < nk_all && kk[j] >= lo) ? 1 : 0;
+        }
         int tot;
-        const int pos = nk + block_scan_flag(ok, sh_int, &tot);
-        if (ok) keys[pos] = kk;
+        int pos = nk + block_scan_i32(cnt, sh_int, &tot);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+            if (i0 + j < nk_all && kk[j] >= lo) keys[pos++] = kk[j];
         nk += tot;
     }
     __syncthreads();
@@ -1869,6 +1891,7 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                             const float ddx = (float)x - (float)(aa & 0xFFFF);
                             const float ddy = (float)y - (float)(aa >> 16);
                             if ((double)(ddx * ddx + ddy * ddy) < md2) {
+                                if (c < 2) cf2[2 * i + c] = (uint16_t)j;
                                 if (c < CONF_K) conf[(int64_t)i * CONF_K + c] = (uint16_t)j;
                                 ++c;
                             }
@@ -1885,7 +1908,13 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                     if (stt[i] != 0) continue;
                     bool blocked = false, rej = false;
                     const int c = ncf[i];
-                    if (c <= CONF_K) {
+                    if (c <= 2) {
+                        for (int k = 0; k < c; ++k) {
+                            const uint8_t sj = stt[cf2[2 * i + k]];
+                            if (sj == 1) { rej = true; break; }
+                            if (sj == 0) blocked = true;
+                        }
+                    } else if (c <= CONF_K) {
                         for (int k = 0; k < c; ++k) {
                             const uint8_t sj = stt[conf[(int64_t)i * CONF_K + k]];
                             if (sj == 1) { rej = true; break; }
@@ -2308,10 +2337,10 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
         S.grid_lds = cells <= GRID_LDS_CELLS ? (int)cells : 0;
         // grid + per-cell candidate lists in LDS when they fit, else in the eigen-map scratch
         // (after the conflict lists) for the same parallel walk, else the wave-serial L2 path
-        if (12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds > 150 * 1024) S.grid_lds = 0;
+        if (16 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds > 150 * 1024) S.grid_lds = 0;
         static const int noglb = [] { const char* e = getenv("VO_SEL_SERIAL_L2"); return e ? atoi(e) : 0; }();
         S.grid_glb = !noglb && S.grid_lds == 0 && SEL_GG_OFF + 2 * cells <= S.gstride;
-        const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
+        const size_t lds = 16 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
         static const bool attr_ok =
             hipFuncSetAttribute((const void*)k_gftt_select<SEL_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 150 * 1024) == hipSuccess &&

@@ -28,7 +28,7 @@ int main()
     S.max_corners = 1400; S.min_dist = 10; S.corners = dcor; S.ncorners = dnc; S.mcap = mcap;
     S.gscratch = dgrid; S.gstride = (int64_t)W * H; S.chain_status = dst;
     S.acc_lds = mcap; S.grid_lds = ((W + 9) / 10) * ((H + 9) / 10);
-    const size_t lds = 12 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
+    const size_t lds = 16 * (size_t)PAGE + 4 * (size_t)S.acc_lds + 8 * (size_t)S.grid_lds;
     CK(hipFuncSetAttribute((const void*)k_gftt_select<SEL_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     std::vector<float> ref(2 * 1400);
