@@ -1839,12 +1839,21 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                 const int y = (int)(addr / (uint32_t)P.W), x = (int)(addr - (uint32_t)y * P.W);
                 cand_xy[i] = (uint32_t)x | ((uint32_t)y << 16);
             }
+            // candidates by cell: with the grid in LDS, a counting sort (head[] = counts, then
+            // start offsets; nxt[] = the candidate indices cell by cell), so a cell's candidates
+            // are read with independent loads; otherwise linked lists in the L2 grid
+            const int ncell = gw * gh;
             if (lds)
-                for (int q = tid; q < gw * gh; q += blockDim.x) head[q] = -1;
+                for (int q = tid; q < ncell; q += blockDim.x) head[q] = 0;
             __syncthreads();
             int* nxt = (int*)page;                                // page keys are dead now
             volatile uint8_t* stt = (volatile uint8_t*)(nxt + PAGE);
-            for (int i = tid; i < take; i += blockDim.x) {
+            constexpr int CPT = PAGE / NT;                        // candidates per thread
+            int slot[CPT];
+#pragma unroll
+            for (int kq = 0; kq < CPT; ++kq) {
+                const int i = tid + kq * NT;
+                if (i >= take) break;
                 const uint32_t xy = cand_xy[i];
                 const int x = (int)(xy & 0xFFFF), y = (int)(xy >> 16);
                 const int xc = x / cs, yc = y / cs;
@@ -1866,9 +1875,44 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                         }
                 }
                 stt[i] = rej ? 2 : 0;                             // 0 undecided, 1 accepted, 2 rejected
-                nxt[i] = lds ? atomicExch(&head[yc * gw + xc], i) : atomicExch(&ghead[yc * gw + xc], i);
+                if (lds) slot[kq] = atomicAdd(&head[yc * gw + xc], 1);
+                else nxt[i] = atomicExch(&ghead[yc * gw + xc], i);
             }
             __syncthreads();
+            if (lds) {
+                // exclusive scan of the cell counts in place, then the cell-ordered index array
+                const int cpt = (ncell + NT - 1) / NT, q0 = tid * cpt, q1 = min(q0 + cpt, ncell);
+                int sum = 0;
+                for (int q = q0; q < q1; ++q) sum += head[q];
+                int tot;
+                int run = block_scan_i32(sum, sh_int, &tot);
+                for (int q = q0; q < q1; ++q) {
+                    const int cnt = head[q];
+                    head[q] = run;
+                    run += cnt;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int kq = 0; kq < CPT; ++kq) {
+                    const int i = tid + kq * NT;
+                    if (i >= take) break;
+                    const uint32_t xy = cand_xy[i];
+                    nxt[head[((int)(xy >> 16) / cs) * gw + (int)(xy & 0xFFFF) / cs] + slot[kq]] = i;
+                }
+                __syncthreads();
+            }
+            // visit(j) for every candidate j in cell cc, until it returns true
+            auto for_cell = [&](int cc, auto&& visit) {
+                if (lds) {
+                    const int e0 = cc + 1 < ncell ? head[cc + 1] : take;
+                    for (int k = head[cc]; k < e0; ++k)
+                        if (visit(nxt[k])) return true;
+                } else {
+                    for (int j = head_get(false, head, ghead, cc); j >= 0; j = nxt[j])
+                        if (visit(j)) return true;
+                }
+                return false;
+            };
             // each candidate's earlier conflicts (same test as OpenCV's walk), found once:
             // count in LDS, indices in the per-chain scratch (the eigen-map buffer, unused on
             // this path); more than CONF_K conflicts -> rescan the cells in every round
@@ -1885,8 +1929,8 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                 int c = 0;
                 for (int yy = y1; yy <= y2; ++yy)
                     for (int xx = x1; xx <= x2; ++xx)
-                        for (int j = head_get(lds, head, ghead, yy * gw + xx); j >= 0; j = nxt[j]) {
-                            if (j >= i) continue;
+                        for_cell(yy * gw + xx, [&](int j) {
+                            if (j >= i) return false;
                             const uint32_t aa = cand_xy[j];
                             const float ddx = (float)x - (float)(aa & 0xFFFF);
                             const float ddy = (float)y - (float)(aa >> 16);
@@ -1895,7 +1939,8 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                                 if (c < CONF_K) conf[(int64_t)i * CONF_K + c] = (uint16_t)j;
                                 ++c;
                             }
-                        }
+                            return false;
+                        });
                 ncf[i] = (uint8_t)min(c, 255);
             }
             __syncthreads();
@@ -1928,18 +1973,19 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
                         const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
                         for (int yy = y1; yy <= y2 && !rej; ++yy)
                             for (int xx = x1; xx <= x2 && !rej; ++xx)
-                                for (int j = head_get(lds, head, ghead, yy * gw + xx); j >= 0; j = nxt[j]) {
-                                    if (j >= i) continue;
+                                for_cell(yy * gw + xx, [&](int j) {
+                                    if (j >= i) return false;
                                     const uint8_t sj = stt[j];
-                                    if (sj == 2) continue;
+                                    if (sj == 2) return false;
                                     const uint32_t aa = cand_xy[j];
                                     const float ddx = (float)x - (float)(aa & 0xFFFF);
                                     const float ddy = (float)y - (float)(aa >> 16);
                                     if ((double)(ddx * ddx + ddy * ddy) < md2) {
-                                        if (sj == 1) { rej = true; break; }
+                                        if (sj == 1) { rej = true; return true; }
                                         blocked = true;
                                     }
-                                }
+                                    return false;
+                                });
                     }
                     if (rej) { stt[i] = 2; changed = true; }
                     else if (!blocked) { stt[i] = 1; changed = true; }
