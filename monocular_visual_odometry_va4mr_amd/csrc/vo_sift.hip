@@ -970,7 +970,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     __shared__ int slist_s[4][64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_kp = im.counters[2];
-    for (int q = blockIdx.x * 4 + w; q < n_kp; q += gridDim.x * 4) {     // wave-uniform loop
+    // cos / sin of every keypoint this wave will describe, one keypoint per lane: the
+    // correctly rounded double-double evaluations (vo_crmath.h) are long serial FP64 chains, so
+    // they run once per wave instead of once per keypoint
+    const int qs = gridDim.x * 4, qf = blockIdx.x * 4 + w;
+    float lane_cos = 0.f, lane_sin = 0.f;
+    {
+        const int ql = qf + lane * qs;
+        if (ql < n_kp) {
+            float angle = 360.f - im.kp_out[6 * (int64_t)ql + 3];
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            lane_cos = (float)vcr_cos((double)(angle * (float)(M_PI / 180)));
+            lane_sin = (float)vcr_sin((double)(angle * (float)(M_PI / 180)));
+        }
+    }
+    int qi = 0;
+    for (int q = qf; q < n_kp; q += qs, ++qi) {                           // wave-uniform loop
         int* pidx = pidx_s[w];
         float* pval = pval_s[w];
         float* hist = hist_s[w];
@@ -993,8 +1008,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const float ori = angle, scl = size * 0.5f;
         const int d = 4, n = 8;
         const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
-        float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
-        float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
+        float cos_t, sin_t;
+        if (qi < 64) {
+            cos_t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lane_cos), qi));
+            sin_t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lane_sin), qi));
+        } else {
+            cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
+            sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
+        }
         const float bins_per_rad = n / 360.f;
         const float exp_scale = -1.f / (d * d * 0.5f);
         const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
