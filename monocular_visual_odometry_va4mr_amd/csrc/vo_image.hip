@@ -1673,6 +1673,19 @@ VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
     else atomicExch(&gg[c], v);
 }
 
+// hist[dgt] += 1 for every lane with `on`, as one atomic per distinct digit of the wave
+VO_DEV void wave_hist_add(int* hist, bool on, int dgt)
+{
+    uint64_t peers = __ballot(on);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        const bool b = (dgt >> bit) & 1;
+        const uint64_t bm = __ballot(b);
+        peers &= b ? bm : ~bm;
+    }
+    if (on && __ffsll((unsigned long long)peers) - 1 == lane_id()) atomicAdd(&hist[dgt], __popcll(peers));
+}
+
 #ifdef VO_SELECT_PROF
 __device__ long long g_selprof[16];
 }  // namespace
@@ -1777,9 +1790,18 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
             for (int shift = 56; shift >= 0; shift -= 8) {
                 for (int q = tid; q < 256; q += blockDim.x) hist[q] = 0;
                 __syncthreads();
-                for (int i = tid; i < nk; i += blockDim.x) {
-                    const uint64_t kk = keys[i];
-                    if ((!has_upper || kk < upper) && (kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255], 1);
+                // four keys per thread per trip (independent loads); one LDS atomic per distinct
+                // digit per wave (peer lanes found with bit-sliced ballots): the keys of a page
+                // mostly share their leading digits, and per-lane atomics on one bin serialised
+                for (int i0 = tid; i0 < nk; i0 += 4 * NT) {
+                    uint64_t kk[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) kk[u] = i0 + u * NT < nk ? keys[i0 + u * NT] : 0ull;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool on = i0 + u * NT < nk && (!has_upper || kk[u] < upper) && (kk[u] & mask) == prefix;
+                        wave_hist_add(hist, on, (int)((kk[u] >> shift) & 255));
+                    }
                 }
                 __syncthreads();
                 if (tid == 0) {
@@ -1801,11 +1823,22 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
         }
         if (tid == 0) sh_int[1] = 0;
         __syncthreads();
-        for (int i = tid; i < nk; i += blockDim.x) {
-            const uint64_t kk = keys[i];
-            if ((!has_upper || kk < upper) && kk >= thr) {
-                const int pos = atomicAdd(&sh_int[1], 1);
-                if (pos < PAGE) page[pos] = kk;
+        for (int i0 = tid; i0 < nk; i0 += 4 * NT) {
+            uint64_t kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) kk[u] = i0 + u * NT < nk ? keys[i0 + u * NT] : 0ull;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                // page order is irrelevant (sorted next): one LDS atomic per wave
+                const bool on = i0 + u * NT < nk && (!has_upper || kk[u] < upper) && kk[u] >= thr;
+                const uint64_t m = __ballot(on);
+                if (m == 0) continue;
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                int base = 0;
+                if (lane_id() == leader) base = atomicAdd(&sh_int[1], __popcll(m));
+                base = __shfl(base, leader, 64);
+                const int pos = base + __popcll(m & ((1ull << lane_id()) - 1ull));
+                if (on && pos < PAGE) page[pos] = kk[u];
             }
         }
         __syncthreads();

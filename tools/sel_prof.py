@@ -2,7 +2,7 @@
 """Phase times of k_gftt_select (block 0 of the launch) on the headline workload: B KITTI
 chains, every stage on one stream.  Needs the diagnostics build
 (make -C monocular_visual_odometry_va4mr_amd/csrc ../_build/libvo_hip_selprof.so).
-usage: python tools/sel_prof.py [B] [steps]"""
+usage: python tools/sel_prof.py [B] [steps] [preset]"""
 import ctypes as C
 import os
 import sys
@@ -21,14 +21,16 @@ from monocular_visual_odometry_va4mr_amd.synth import Renderer, poses  # noqa: E
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 384
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+preset = sys.argv[3] if len(sys.argv) > 3 else "kitti"
 dev = torch.device("cuda")
-r = Renderer("kitti", seed=1, device=dev)
-opts, (b0, b1), n_seq = Op.get("kitti")
+r = Renderer(preset, seed=1, device=dev)
+opts, (b0, b1), n_seq = Op.get(preset)
 n = steps + b1 + 2
-Rs, cs = poses(4541, r.p)
-starts = [(i * (4541 - n)) // max(1, B) for i in range(B)]
+Rs, cs = poses(n_seq, r.p)
+starts = [(i * (n_seq - n)) // max(1, B) for i in range(B)]
 frames = torch.stack([r.render_batch(list(range(s, s + n)), Rs[s:s + n], cs[s:s + n]) for s in starts], 1)
-eng = Engine(r.K, opts, r.W, r.H, batch=B, device=dev, ncap=16384, pcap=16384, fcap=n + 8)
+cap = 65536 if preset == "hd1080" else 16384
+eng = Engine(r.K, opts, r.W, r.H, batch=B, device=dev, ncap=cap, pcap=cap, fcap=n + 8)
 eng.bootstrap(frames[b0], frames[b1])
 lib = L.lib()
 lib.vo_select_prof_read.argtypes = [C.c_void_p]
