@@ -1673,6 +1673,19 @@ VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
     else atomicExch(&gg[c], v);
 }
 
+// the same for 12-bit digits
+VO_DEV void wave_hist_add12(int* hist, bool on, int dgt)
+{
+    uint64_t peers = __ballot(on);
+#pragma unroll
+    for (int bit = 0; bit < 12; ++bit) {
+        const bool b = (dgt >> bit) & 1;
+        const uint64_t bm = __ballot(b);
+        peers &= b ? bm : ~bm;
+    }
+    if (on && __ffsll((unsigned long long)peers) - 1 == lane_id()) atomicAdd(&hist[dgt], __popcll(peers));
+}
+
 // hist[dgt] += 1 for every lane with `on`, as one atomic per distinct digit of the wave
 VO_DEV void wave_hist_add(int* hist, bool on, int dgt)
 {
@@ -1718,6 +1731,7 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
     __shared__ uint32_t round_xy[64];
     __shared__ int hist[256];
     __shared__ int sh_int[16];
+    __shared__ int sh_scan[16];
     __shared__ uint64_t sh_u64[4];
     const int b = blockIdx.x;
     if (P.chain_status[b] != 0) return;
@@ -1785,14 +1799,17 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
         uint64_t thr = 0;
         const int take = remaining < PAGE ? remaining : PAGE;
         if (remaining > PAGE) {
+            // radix select of the PAGE-th largest key, 12-bit digits (histogram in the page
+            // buffer, free until the gather): usually three passes over the keys instead of eight
             uint64_t prefix = 0, mask = 0;
             int k = PAGE;
-            for (int shift = 56; shift >= 0; shift -= 8) {
-                for (int q = tid; q < 256; q += blockDim.x) hist[q] = 0;
+            int* hist4 = (int*)page;
+            for (int shift = 52; shift >= -8; shift -= 12) {
+                const int sh = shift < 0 ? 0 : shift;                      // last digit: bits 3..0
+                const int dbits = shift < 0 ? 4 : 12;
+                const uint64_t dmask = ((uint64_t)1 << dbits) - 1;
+                for (int q = tid; q < 4096; q += NT) hist4[q] = 0;
                 __syncthreads();
-                // four keys per thread per trip (independent loads); one LDS atomic per distinct
-                // digit per wave (peer lanes found with bit-sliced ballots): the keys of a page
-                // mostly share their leading digits, and per-lane atomics on one bin serialised
                 for (int i0 = tid; i0 < nk; i0 += 4 * NT) {
                     uint64_t kk[4];
 #pragma unroll
@@ -1800,26 +1817,40 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const bool on = i0 + u * NT < nk && (!has_upper || kk[u] < upper) && (kk[u] & mask) == prefix;
-                        wave_hist_add(hist, on, (int)((kk[u] >> shift) & 255));
+                        wave_hist_add12(hist4, on, (int)((kk[u] >> sh) & dmask));
                     }
                 }
                 __syncthreads();
-                if (tid == 0) {
-                    int cum = 0, dsel = 0;
-                    for (int dgt = 255; dgt >= 0; --dgt) {
-                        if (cum + hist[dgt] >= k) { dsel = dgt; break; }
-                        cum += hist[dgt];
+                // the digit holding the k-th largest: descending digit order over the threads,
+                // NT / 4096-bin slices, one block scan
+                constexpr int BPT = 4096 / NT;
+                const int hi = 4095 - tid * BPT;
+                int loc = 0;
+#pragma unroll
+                for (int j = 0; j < BPT; ++j) loc += hist4[hi - j];
+                int tot;
+                const int before = block_scan_i32(loc, sh_scan, &tot);
+                if (before < k && k <= before + loc) {
+                    int cum = before;
+                    for (int j = 0; j < BPT; ++j) {
+                        const int h = hist4[hi - j];
+                        if (cum + h >= k) {
+                            sh_u64[0] = prefix | ((uint64_t)(hi - j) << sh);
+                            sh_int[0] = k - cum;
+                            sh_int[1] = h;
+                            break;
+                        }
+                        cum += h;
                     }
-                    sh_u64[0] = prefix | ((uint64_t)dsel << shift);
-                    sh_int[0] = k - cum;
                 }
                 __syncthreads();
                 prefix = sh_u64[0];
                 k = sh_int[0];
-                mask |= (uint64_t)0xFF << shift;
+                const int in_bucket = sh_int[1];
+                mask |= dmask << sh;
                 __syncthreads();
-            }
-            thr = prefix;
+                if (in_bucket == k) break;          // the whole bucket is in: prefix (low bits 0) is the threshold
+            }            thr = prefix;
         }
         if (tid == 0) sh_int[1] = 0;
         __syncthreads();
@@ -2431,9 +2462,11 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
         // block size SEL_THREADS = 512, or VO_SEL_THREADS = 256 / 1024 (same result).  Headline
         // bench: 512 threads 56.2k frames/s, 1024 55.1k, 256 55.9k -- a select block holds its
         // wave slots while the other stream group's LK runs
-        static const int nt_env = [] { const char* e = getenv("VO_SEL_THREADS"); return e ? atoi(e) : SEL_THREADS; }();
-        if (nt_env == 256) hipLaunchKernelGGL(k_gftt_select<256>, dim3(d->B), dim3(256), lds, st, S);
-        else if (nt_env == 1024) hipLaunchKernelGGL(k_gftt_select<1024>, dim3(d->B), dim3(1024), lds, st, S);
+        static const int nt_env = [] { const char* e = getenv("VO_SEL_THREADS"); return e ? atoi(e) : 0; }();
+        // few chains (the GPU is mostly idle during the select): 1024 threads per chain
+        const int nt_sel = nt_env ? nt_env : (d->B <= 128 ? 1024 : SEL_THREADS);
+        if (nt_sel == 256) hipLaunchKernelGGL(k_gftt_select<256>, dim3(d->B), dim3(256), lds, st, S);
+        else if (nt_sel == 1024) hipLaunchKernelGGL(k_gftt_select<1024>, dim3(d->B), dim3(1024), lds, st, S);
         else hipLaunchKernelGGL(k_gftt_select<SEL_THREADS>, dim3(d->B), dim3(SEL_THREADS), lds, st, S);
     }
     return hip_ok() ? VO_OK : VO_EHIP;
