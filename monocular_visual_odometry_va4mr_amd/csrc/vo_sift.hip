@@ -968,6 +968,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     __shared__ float red_s[4][2];
     __shared__ uint32_t ring_s[4][128];
     __shared__ int slist_s[4][64];
+    // exp32f's 64-entry table in LDS (a gather per pixel: no global round trip)
+    __shared__ float tab_s[64];
+    if (threadIdx.x < 64) tab_s[threadIdx.x] = sb.consts[EXPTAB_OFF + threadIdx.x];
+    __syncthreads();
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_kp = im.counters[2];
     // cos / sin of every keypoint this wave will describe, one keypoint per lane: the
@@ -992,7 +996,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         float* dsl = dst_s[w];
         uint32_t* ring = ring_s[w];
         int* slist = slist_s[w];
-        const float* tab = sb.consts + EXPTAB_OFF;
+        const float* tab = tab_s;
         const float* kp = im.kp_out + 6 * (int64_t)q;
         const int kpo = (int)kp[5];
         int octave = kpo & 255, layer = (kpo >> 8) & 255;
