@@ -45,6 +45,22 @@ def test_c5_gftt_bitexact(hd_frames):
     assert np.array_equal(got, ref)
 
 
+def test_gftt_capacity_is_reported_not_truncated(hd_frames):
+    """More corners wanted than the engine holds (maxCorners 0 = unlimited; the corner buffer is
+    8,192): the selection reports the overflow (nCorners = -1, which k_add_finish turns into
+    VO_ST_CAPACITY) instead of returning a silently truncated list."""
+    from oracle import _olib as O
+    fr, K = hd_frames
+    eng, opts = _engine(K, 1920, 1080, feature_max_corners=0, feature_quality_level=0.001, feature_min_dist=1)
+    assert eng.dims.mcap == 8192
+    eng.build_pyramid(fr[1], 0)
+    assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+    torch.cuda.synchronize()
+    ref = O.gftt(fr[1], 0, 0.001, 1, 3)
+    assert len(ref) > 8192
+    assert int(eng.t["nCorners"][0]) == -1
+
+
 def test_c5_lk_bitexact(hd_frames):
     """KLT on ~12.7k points at 1080p: GFTT corners of frame 0 plus jittered copies (the
     candidate + landmark load of a C5 step), tracked 0 -> 1."""
