@@ -1598,7 +1598,8 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
         if (ir >= g0 + 1) {
             const int pr = ir - 1;                       // gradient row
             const int gx = hdA + 2 * hdB + hd, gy = hs - hsA;
-            const int pxx = gx * gx, pxy = gx * gy, pyy = gy * gy;
+            // |gx|, |gy| <= 4 * 255: 24-bit multiplies (full rate; v_mul_lo_u32 is quarter rate)
+            const int pxx = __mul24(gx, gx), pxy = __mul24(gx, gy), pyy = __mul24(gy, gy);
             int lxx = dpp_from_left(pxx), lxy = dpp_from_left(pxy), lyy = dpp_from_left(pyy);
             int rxx = dpp_from_right(pxx), rxy = dpp_from_right(pxy), ryy = dpp_from_right(pyy);
             if (hedge) {                                 // boxFilter BORDER_REFLECT_101 in x
