@@ -92,7 +92,7 @@ class VisualOdometryPipeLine:
         else:
             eng.step(img[None])
         self._frame = img
-        st, n_inl = eng.status_word()                          # one host sync per frame
+        st, n_inl = eng.status_word(in_graph=self._use_graph)  # one host sync per frame
         if st == L.ST_OK:
             if len(self.num_tracked_landmarks_list) == 20:     # :360-364
                 self.num_tracked_landmarks_list.pop(0)

@@ -201,15 +201,19 @@ class Engine:
     def statuses(self) -> np.ndarray:
         return self.t["status"].cpu().numpy()
 
-    def status_word(self) -> tuple[int, int]:
-        """(status, inlier count) of chain 0 with one host synchronisation: both gathered on
-        the device, one copy into a pinned host word (the drop-in class reads them after
-        every frame)."""
+    def _sw_alloc(self):
         if getattr(self, "_sw_host", None) is None:
             self._sw_dev = torch.zeros(2, dtype=torch.int32, device=self.device)
             self._sw_host = torch.zeros(2, dtype=torch.int32).pin_memory()
-        torch.cat([self.t["status"][:1], self.t["nInl"][:1]], out=self._sw_dev)
-        self._sw_host.copy_(self._sw_dev, non_blocking=True)
+
+    def status_word(self, in_graph: bool = False) -> tuple[int, int]:
+        """(status, inlier count) of chain 0 with one host synchronisation: both gathered on
+        the device, one copy into a pinned host word (the drop-in class reads them after
+        every frame).  ``in_graph``: the last replayed step graph already wrote the word."""
+        self._sw_alloc()
+        if not in_graph:
+            torch.cat([self.t["status"][:1], self.t["nInl"][:1]], out=self._sw_dev)
+            self._sw_host.copy_(self._sw_dev, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         return int(self._sw_host[0]), int(self._sw_host[1])
 
@@ -302,6 +306,7 @@ class Engine:
         """Capture the two ping-pong variants of the step into hipGraphs; returns a
         replay function taking a device frame buffer already bound at capture time."""
         buf = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=self.device)
+        self._sw_alloc()
         graphs = []
         side = torch.cuda.Stream(self.device)
         for prev in (0, 1):
@@ -309,6 +314,10 @@ class Engine:
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
                     self._step_launch(buf, prev)
+                    # the status word of chain 0 as the graph's last nodes: gathered on the
+                    # device and copied into pinned host memory (status_word then only waits)
+                    torch.cat([self.t["status"][:1], self.t["nInl"][:1]], out=self._sw_dev)
+                    self._sw_host.copy_(self._sw_dev, non_blocking=True)
             graphs.append(g)
         torch.cuda.synchronize(self.device)
         self._graphs = {"buf": buf, "g": graphs}
