@@ -1674,7 +1674,8 @@ VO_DEV void cell_set(bool lds, uint32_t* lg, uint32_t* gg, int c, uint32_t v)
     else atomicExch(&gg[c], v);
 }
 
-// the same for 12-bit digits
+// hist[dgt] += 1 for every lane with `on` (12-bit digits), as one LDS atomic per distinct digit
+// of the wave: peer lanes found with bit-sliced ballots
 VO_DEV void wave_hist_add12(int* hist, bool on, int dgt)
 {
     uint64_t peers = __ballot(on);
@@ -1687,18 +1688,6 @@ VO_DEV void wave_hist_add12(int* hist, bool on, int dgt)
     if (on && __ffsll((unsigned long long)peers) - 1 == lane_id()) atomicAdd(&hist[dgt], __popcll(peers));
 }
 
-// hist[dgt] += 1 for every lane with `on`, as one atomic per distinct digit of the wave
-VO_DEV void wave_hist_add(int* hist, bool on, int dgt)
-{
-    uint64_t peers = __ballot(on);
-#pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-        const bool b = (dgt >> bit) & 1;
-        const uint64_t bm = __ballot(b);
-        peers &= b ? bm : ~bm;
-    }
-    if (on && __ffsll((unsigned long long)peers) - 1 == lane_id()) atomicAdd(&hist[dgt], __popcll(peers));
-}
 
 #ifdef VO_SELECT_PROF
 __device__ long long g_selprof[16];
@@ -1730,7 +1719,6 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
     // its list (up to CONF_K) is in the per-chain global scratch
     uint16_t* cf2 = (uint16_t*)(head + P.grid_lds);
     __shared__ uint32_t round_xy[64];
-    __shared__ int hist[256];
     __shared__ int sh_int[16];
     __shared__ int sh_scan[16];
     __shared__ uint64_t sh_u64[4];

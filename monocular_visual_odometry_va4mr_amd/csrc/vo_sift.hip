@@ -919,29 +919,17 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
 //    math, in parallel); the valid ones are compacted into LDS in raster order;
 //  * the histogram (360 bins) lives in LDS.  The eight bins a pixel touches
 //    (idx + {0, 1, 10, 11, 60, 61, 70, 71}) are distinct, so eight lanes update them with one
-//    read-add-write; pixels follow in raster order (lds_rmw_add_lanes), so each bin receives
+//    read-add-write; pixels follow in raster order (lds_rmw_add4_lanes), so each bin receives
 //    its additions in exactly the serial order;
 //  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
-// Histogram update of the descriptor walk, written as asm with exec narrowed to one pixel's
-// lanes: straight-line code (no branch per pixel).  A wave's LDS operations execute in issue
-// order, so the next pixel's read sees this write.  (ds_add_f32 on the same lanes is exact too
-// but measured 4x slower: LDS float atomics run at a fraction of the read/write rate.)
-// hist[p] += v for the lanes in `lanes` (wave-uniform): plain LDS read, v_add_f32, write.
-VO_DEV void lds_rmw_add_lanes(float* p, float v, uint64_t lanes)
-{
-    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
-    uint64_t save;
-    float h;
-    asm volatile("s_mov_b64 %0, exec\n\ts_and_b64 exec, exec, %4\n\tds_read_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\t"
-                 "v_add_f32 %1, %1, %3\n\tds_write_b32 %2, %1\n\ts_mov_b64 exec, %0"
-                 : "=&s"(save), "=&v"(h)
-                 : "v"(a), "v"(v), "s"(lanes)
-                 : "memory");
-}
-
-// The same for a run of up to four pixels with the same eight bins: one read, the four adds in
-// pixel order (missing pixels add +0, which leaves a bin unchanged: every contribution and
-// every partial sum is >= +0), one write.
+// Histogram update of the descriptor walk: hist[p] += v0, v1, v2, v3 in that order for the
+// lanes in `lanes` (wave-uniform), i.e. a run of up to four pixels with the same eight bins --
+// one read, the four adds in pixel order (missing pixels add +0, which leaves a bin unchanged:
+// every contribution and every partial sum is >= +0), one write.  Written as asm with exec
+// narrowed to the run's lanes: straight-line code, no branch per run.  A wave's LDS operations
+// execute in issue order, so the next run's read sees this write.  (ds_add_f32 on the same
+// lanes is exact too but measured 4x slower: LDS float atomics run at a fraction of the
+// read/write rate.)
 VO_DEV void lds_rmw_add4_lanes(float* p, float v0, float v1, float v2, float v3, uint64_t lanes)
 {
     const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
@@ -955,7 +943,7 @@ VO_DEV void lds_rmw_add4_lanes(float* p, float v0, float v1, float v2, float v3,
                  : "memory");
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_sift_desc_w(vo_sift_buf sb)
+__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
