@@ -234,6 +234,107 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
     }
 }
 
+// k_blur_tile for a compile-time kernel size N (the SIFT sizes 11, 13, 17, 21, 27), same
+// tile, same staging, same tap order -- on packed FP32 (v_pk_mul_f32 / v_pk_add_f32: two
+// independent IEEE operations per lane, rounded exactly as the scalar pair):
+//  * taps in scalar registers (uniform loads of `kern`), no per-tap LDS read;
+//  * row pass: a thread sums two rows x four columns, the pair of rows in one packed register
+//    ({row y, row y+1} of each source column), N + 3 reads per row;
+//  * column pass: a thread sums two columns x four rows, the column pair read as one 8-byte
+//    LDS load per source row.
+// One packed multiply + one packed add per tap per two outputs (the scalar form: two each).
+typedef float vf2 __attribute__((ext_vector_type(2)));
+template <int N>
+__global__ void __launch_bounds__(256) k_blur_tile_n(const float* __restrict__ src, int64_t src_stride,
+                                                     float* __restrict__ dst, int64_t dst_stride,
+                                                     float* __restrict__ dog, int64_t dog_stride, int w, int h,
+                                                     const float* __restrict__ kern)
+{
+    constexpr int r = N >> 1;
+    constexpr int rows = BT_H + 2 * r, cols = BT_W + 2 * r, sst = cols + 1;
+    static_assert(r <= BT_R && rows % 2 == 0, "k_blur_tile_n tile");
+    __shared__ float s_src[rows * sst];
+    __shared__ __attribute__((aligned(16))) float s_row[rows * BT_W];
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
+    src += blockIdx.z * src_stride;
+    dst += blockIdx.z * dst_stride;
+    float kk[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) kk[k] = kern[k];
+    {
+        constexpr int NR = (rows + 3) / 4, NC = (cols + 63) / 64;
+        const int lx = tid & 63, wy = tid >> 6;
+        int xo[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) xo[c] = refl101(x0 - r + min(lx + 64 * c, cols - 1), w);
+        float v[NR][NC];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int ty = min(wy + 4 * j, rows - 1);
+            const float* srow = src + (int64_t)refl101(y0 - r + ty, h) * w;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) v[j][c] = srow[xo[c]];
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int ty = wy + 4 * j;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int tx = lx + 64 * c;
+                if (ty < rows && tx < cols) s_src[ty * sst + tx] = v[j][c];
+            }
+        }
+    }
+    __syncthreads();
+    // row pass: item = rows (2 q, 2 q + 1) x columns 4 c .. 4 c + 3
+    for (int i = tid; i < (rows / 2) * (BT_W / 4); i += 256) {
+        const int ty = 2 * (i >> 4), tx = (i & 15) * 4;
+        const float* sp = s_src + ty * sst + tx;
+        vf2 v[N + 3];
+#pragma unroll
+        for (int m = 0; m < N + 3; ++m) v[m] = vf2{sp[m], sp[sst + m]};
+        vf2 a0 = {0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const vf2 kv = {kk[k], kk[k]};
+            a0 = a0 + kv * v[k]; a1 = a1 + kv * v[k + 1]; a2 = a2 + kv * v[k + 2]; a3 = a3 + kv * v[k + 3];
+        }
+        *reinterpret_cast<float4*>(s_row + ty * BT_W + tx) = make_float4(a0.x, a1.x, a2.x, a3.x);
+        *reinterpret_cast<float4*>(s_row + (ty + 1) * BT_W + tx) = make_float4(a0.y, a1.y, a2.y, a3.y);
+    }
+    __syncthreads();
+    // column pass: columns (2 c, 2 c + 1) x rows 4 g .. 4 g + 3
+    {
+        const int tx = 2 * (tid & 31), ty = (tid >> 5) * 4;
+        const float* sp = s_row + ty * BT_W + tx;
+        vf2 v[N + 3];
+#pragma unroll
+        for (int m = 0; m < N + 3; ++m) v[m] = *reinterpret_cast<const vf2*>(sp + m * BT_W);
+        vf2 a[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const vf2 kv = {kk[k], kk[k]};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = a[j] + kv * v[k + j];
+        }
+        const int gx = x0 + tx;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int gy = y0 + ty + j;
+            if (gy >= h) continue;
+            const float* cs = s_src + (ty + j + r) * sst + tx + r;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                if (gx + e >= w) continue;
+                const float o = e ? a[j].y : a[j].x;
+                dst[(int64_t)gy * w + gx + e] = o;
+                if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx + e] = o - cs[e];
+            }
+        }
+    }
+}
+
 __global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst, int dw, int dh,
                           int64_t stride)
 {
@@ -921,7 +1022,10 @@ __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
 //    (idx + {0, 1, 10, 11, 60, 61, 70, 71}) are distinct, so eight lanes update them with one
 //    read-add-write; pixels follow in raster order (lds_rmw_add4_lanes), so each bin receives
 //    its additions in exactly the serial order;
-//  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane.
+//  * the 128-entry normalisation sums stay sequential (lane 0), clamps / scaling run per lane;
+//  * 8 waves per SIMD: the 128-float descriptor row reuses the contribution buffer (19.7 KB of
+//    LDS per 4-wave block) and VGPRs are capped at 64 -- the walk is LDS-latency bound, so the
+//    extra waves pay for the few per-keypoint spills (batch-64 KITTI desc -15 %).
 // Histogram update of the descriptor walk: hist[p] += v0, v1, v2, v3 in that order for the
 // lanes in `lanes` (wave-uniform), i.e. a run of up to four pixels with the same eight bins --
 // one read, the four adds in pixel order (missing pixels add +0, which leaves a bin unchanged:
@@ -943,7 +1047,7 @@ VO_DEV void lds_rmw_add4_lanes(float* p, float v0, float v1, float v2, float v3,
                  : "memory");
 }
 
-__global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_sift_desc_w(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
     __shared__ int4 pidx_s4[4][16];
@@ -952,7 +1056,6 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
     // lanes) and the walk's loads (lane 8j + k reads pixel g + j's k-th) are conflict-free
     __shared__ float pval_s[4][8 * 72];
     __shared__ float hist_s[4][384];
-    __shared__ float dst_s[4][128];
     __shared__ float red_s[4][2];
     __shared__ uint32_t ring_s[4][128];
     __shared__ int slist_s[4][64];
@@ -981,7 +1084,7 @@ __global__ void __launch_bounds__(256) k_sift_desc_w(vo_sift_buf sb)
         int* pidx = pidx_s[w];
         float* pval = pval_s[w];
         float* hist = hist_s[w];
-        float* dsl = dst_s[w];
+        float* dsl = pval_s[w];       // the walk's contributions are dead once it ends
         uint32_t* ring = ring_s[w];
         int* slist = slist_s[w];
         const float* tab = tab_s;
@@ -1381,10 +1484,21 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
                        sb->tmp, sb->tmp_floats);
     auto blur = [&](const float* src, int64_t src_stride, float* dst, float* dog, int w, int h, int layer) {
         dim3 g((w + BT_W - 1) / BT_W, (h + BT_H - 1) / BT_H, nb);
+        const float* kern = sb->consts + layer * KTAPS;
+        // packed compile-time-size form for the SIFT kernel sizes (VO_SIFT_BLUR_GENERIC=1: the
+        // runtime-size kernel; both identical)
+        static const bool generic = [] { const char* e = getenv("VO_SIFT_BLUR_GENERIC"); return e && atoi(e) == 1; }();
+        switch (generic ? 0 : ks[layer]) {
+        case 11: hipLaunchKernelGGL(k_blur_tile_n<11>, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h, kern); return;
+        case 13: hipLaunchKernelGGL(k_blur_tile_n<13>, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h, kern); return;
+        case 17: hipLaunchKernelGGL(k_blur_tile_n<17>, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h, kern); return;
+        case 21: hipLaunchKernelGGL(k_blur_tile_n<21>, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h, kern); return;
+        case 27: hipLaunchKernelGGL(k_blur_tile_n<27>, g, dim3(256), 0, st, src, src_stride, dst, gs, dog, ds, w, h, kern); return;
+        default: break;
+        }
         const int rr = ks[layer] >> 1;
         const size_t lds = sizeof(float) * (size_t)(BT_H + 2 * rr) * (BT_W + 2 * rr + 1 + BT_W);
-        hipLaunchKernelGGL(k_blur_tile, g, dim3(256), lds, st, src, src_stride, dst, gs, dog, ds, w, h,
-                           (const float*)(sb->consts + layer * KTAPS), ks[layer]);
+        hipLaunchKernelGGL(k_blur_tile, g, dim3(256), lds, st, src, src_stride, dst, gs, dog, ds, w, h, kern, ks[layer]);
     };
     blur(sb->tmp, sb->tmp_floats, sb->gauss + sb->gauss_off[0], nullptr, 2 * W, 2 * H, 0);
     for (int o = 0; o < sb->n_oct; ++o) {
