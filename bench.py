@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stagger", type=int, default=0, help="1: start the groups out of phase (see main)")
+    ap.add_argument("--lookahead", type=int, default=int(os.environ.get("VO_LOOKAHEAD", "0")),
+                    help="1: each step builds the next frame's pyramid (Engine.step_ahead; measured slower, see DESIGN); 0: its own")
     ap.add_argument("--cu-reserve", type=int, default=int(os.environ.get("VO_CU_RESERVE", "0")),
                     help="launch LK on a CU-masked stream per group that leaves this many CUs free "
                          "for the other groups' latency-bound stages (0: off)")
@@ -422,10 +424,19 @@ def main():
     torch.cuda.synchronize()
     boot_s = time.perf_counter() - t0
 
+    last = frames.shape[0] - 1
+
     def step_all(j, marks=None):
         for g, e in enumerate(engines):
             with torch.cuda.stream(streams[g]):
-                e.step(frames[j, bounds[g]:bounds[g + 1]], marks=marks if g == 0 else None)
+                mk = marks if g == 0 else None
+                if args.lookahead:
+                    # one frame of pyramid lookahead: step j also builds frame j+1's pyramid
+                    # (the last step rebuilds its own frame's: the same work per step)
+                    e.step_ahead(frames[j, bounds[g]:bounds[g + 1]],
+                                 frames[min(j + 1, last), bounds[g]:bounds[g + 1]], marks=mk)
+                else:
+                    e.step(frames[j, bounds[g]:bounds[g + 1]], marks=mk)
 
     # --stagger: group g starts its first step only when group g-1's first `track` stage has
     # ended, so the groups run out of phase: one group's latency-bound stages (PnP, select,
@@ -573,7 +584,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": "C2 kitti seq00-length synthetic 1241x376, per-frame continuous_operation",
                    "width": Wd, "height": H, "chains_per_gpu": B, "frames_per_step": world * B,
-                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "cu_reserve": args.cu_reserve, "seq_len": SEQ_LEN,
+                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "cu_reserve": args.cu_reserve, "pyramid_lookahead": args.lookahead, "seq_len": SEQ_LEN,
                    "seed": args.seed},
         "roofline": roof,
         "roofline_valu": roof_valu,

@@ -45,6 +45,26 @@ VO_DEV int wave_sum_dpp(int x)
     return __builtin_amdgcn_readlane(x, 63);
 }
 
+// Two wave sums with their DPP steps interleaved: each step's two adds are independent, so the
+// chain issues back to back instead of waiting out the DPP read hazard of one reduction.
+VO_DEV void wave_sum2_dpp(int& x, int& y)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0xB1, 0xF, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0x4E, 0xF, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0x124, 0xF, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0x128, 0xF, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0x142, 0xA, 0xF, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);
+    y += __builtin_amdgcn_update_dpp(0, y, 0x143, 0xC, 0xF, false);
+    x = __builtin_amdgcn_readlane(x, 63);
+    y = __builtin_amdgcn_readlane(y, 63);
+}
+
 // Exact wave-wide sum of per-lane int32 partials whose total may exceed 32 bits:
 // p = hi * 2^16 + lo with lo in [0, 65535]; both halves sum exactly in int32 over 64 lanes.
 VO_DEV int64_t wave_sum_split(int p)

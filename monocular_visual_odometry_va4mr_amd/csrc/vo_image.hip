@@ -929,7 +929,7 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
                                                (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
                     // int32 -> float and int64 -> float round the same integer identically
                     float fb1, fb2;
-                    if (!wide) { fb1 = (float)wave_sum_dpp(b1) * FLT_SCALE; fb2 = (float)wave_sum_dpp(b2) * FLT_SCALE; }
+                    if (!wide) { wave_sum2_dpp(b1, b2); fb1 = (float)b1 * FLT_SCALE; fb2 = (float)b2 * FLT_SCALE; }
                     else { fb1 = (float)wave_sum_split(b1) * FLT_SCALE; fb2 = (float)wave_sum_split(b2) * FLT_SCALE; }
                     const float ddx = (A12 * fb2 - A22 * fb1) * D;
                     const float ddy = (A12 * fb1 - A11 * fb2) * D;

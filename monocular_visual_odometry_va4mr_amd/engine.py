@@ -255,7 +255,54 @@ class Engine:
             self._side = torch.cuda.Stream(self.device, priority=getattr(self, "side_priority", 0))
         return self._side
 
-    def _step_launch(self, frames, prev, marks=None):
+    # ------------------------------------------------------------------ pyramid lookahead
+    def step_ahead(self, frames, frames_next, marks=None):
+        """step(frames) with one frame of pyramid lookahead (a streaming pipeline): this frame's
+        pyramid + Scharr derivatives were built during the previous step, and the pyramid of
+        ``frames_next`` is built during this one, on the GFTT side stream ahead of this frame's
+        GFTT.  Every step still builds exactly one pyramid; tracking then never waits for the
+        new frame's pyramid, which otherwise runs between two LK launches.  Three physical
+        pyramid buffers rotate through the roles previous / current / next; the state's
+        pyr[0] / pyr[1] are re-pointed before every step (prev = 0), so ``self.prev`` and the
+        state keep their usual meaning between steps.  Results are identical to step()."""
+        frames = self._frames(frames)
+        frames_next = self._frames(frames_next)
+        T = self.t
+        if getattr(self, "_la", None) is None:
+            for k in ("pyr", "der"):
+                T[k + "2"] = torch.zeros_like(T[k + "0"])
+            la = L.VoState()
+            for name in L._STATE_FIELDS:
+                setattr(la, name, getattr(self.state, name))
+            # physical buffers in the roles (prev, cur, next); prev holds potential_frame
+            roles = [self.prev, 1 - self.prev, 2]
+            self._la = {"state": la, "ps": C.byref(la), "roles": roles, "ready": None, "frames": None}
+            # prologue: this frame's pyramid into the `cur` buffer, in stream order
+            self._la_point(la, 0, roles[1])
+            self._chk(self.lib.vo_pyr_build(self._pd, self._la["ps"], 0, C.c_void_p(frames.data_ptr()),
+                                            self.W * self.H, self.stream), "vo_pyr_build")
+        st = self._la
+        roles = st["roles"]
+        main = torch.cuda.current_stream(self.device)
+        if st["ready"] is not None:
+            main.wait_event(st["ready"])                 # this frame's pyramid (built last step)
+        self._la_point(self.state, 0, roles[0])
+        self._la_point(self.state, 1, roles[1])
+        self._la_point(st["state"], 0, roles[2])
+        st["frames"] = frames_next                       # alive until the side stream used it
+        self._step_launch(frames, 0, marks, ahead=frames_next)
+        st["roles"] = [roles[1], roles[2], roles[0]]
+        self.prev = 0
+        # between steps the state shows (potential_frame, next frame) as pyr[0], pyr[1]
+        self._la_point(self.state, 0, st["roles"][0])
+        self._la_point(self.state, 1, st["roles"][1])
+
+    def _la_point(self, state, slot, phys):
+        T = self.t
+        setattr(state, "pyr%d" % slot, T["pyr%d" % phys].data_ptr())
+        setattr(state, "der%d" % slot, T["der%d" % phys].data_ptr())
+
+    def _step_launch(self, frames, prev, marks=None, ahead=None):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
         new frame (pyr[cur], der[cur]) -> track(prev) -> PnP -> triangulate -> [join] ->
         add_finish.  side: GFTT on the new frame (needs only its pyramid,
@@ -278,9 +325,30 @@ class Engine:
                 marks(i, True, strm)
 
         forked = side.cuda_stream != main.cuda_stream
-        run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
-        if forked:
-            side.wait_stream(main)                                # pyramid(cur) ready
+        if ahead is None:
+            run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
+            if forked:
+                side.wait_stream(main)                            # pyramid(cur) ready
+        else:
+            # lookahead: pyr(cur) is ready (step_ahead waited for it); the next frame's pyramid
+            # goes into the buffer the previous step's tracking released, on the side stream
+            # ahead of this frame's GFTT
+            if forked:
+                side.wait_stream(main)
+            la = self._la
+            fn = C.c_void_p(ahead.data_ptr())
+            # VO_LA_STREAM=own: on a stream of its own (GFTT does not wait for it)
+            if forked and os.environ.get("VO_LA_STREAM") == "own":
+                if la.get("stream") is None:
+                    la["stream"] = torch.cuda.Stream(self.device)
+                ls = la["stream"]
+                ls.wait_stream(main)
+            else:
+                ls = side
+            run(0, ls, lambda: lib.vo_pyr_build(pd, la["ps"], 0, fn, self.W * self.H, C.c_void_p(ls.cuda_stream)))
+            ev = torch.cuda.Event()
+            ev.record(ls)
+            la["ready"] = ev
         run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         bulk = getattr(self, "bulk_stream", None)
         if bulk is not None:
