@@ -65,6 +65,19 @@ VO_DEV void wave_sum2_dpp(int& x, int& y)
     y = __builtin_amdgcn_readlane(y, 63);
 }
 
+VO_DEV void wave_sum3_dpp(int& x, int& y, int& z)
+{
+#define VO_DPP3(ctl, rm) \
+    x += __builtin_amdgcn_update_dpp(0, x, ctl, rm, 0xF, false); \
+    y += __builtin_amdgcn_update_dpp(0, y, ctl, rm, 0xF, false); \
+    z += __builtin_amdgcn_update_dpp(0, z, ctl, rm, 0xF, false);
+    VO_DPP3(0xB1, 0xF) VO_DPP3(0x4E, 0xF) VO_DPP3(0x124, 0xF) VO_DPP3(0x128, 0xF) VO_DPP3(0x142, 0xA) VO_DPP3(0x143, 0xC)
+#undef VO_DPP3
+    x = __builtin_amdgcn_readlane(x, 63);
+    y = __builtin_amdgcn_readlane(y, 63);
+    z = __builtin_amdgcn_readlane(z, 63);
+}
+
 // Exact wave-wide sum of per-lane int32 partials whose total may exceed 32 bits:
 // p = hi * 2^16 + lo with lo in [0, 65535]; both halves sum exactly in int32 over 64 lanes.
 VO_DEV int64_t wave_sum_split(int p)

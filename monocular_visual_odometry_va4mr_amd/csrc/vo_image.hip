@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
         float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
         for (level = level_hi; level >= level_lo; --level) {
         cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level]; loff = (int)P.loff[level];
-        const float sc = (float)(1. / (1 << level));
+        const float sc = __builtin_ldexpf(1.f, -level);     // 1 / 2^level, exact (no f64 division)
         float px = ptx * sc, py = pty * sc;
         if (level == P.L) { ox = px; oy = py; }
         else if (level == level_hi) {
@@ -866,8 +866,8 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
                 const float FLT_SCALE = 1.f / (1 << 20);
                 float A11, A12, A22;
                 if (!twide) {
-                    A11 = (float)wave_sum_dpp(a11) * FLT_SCALE; A12 = (float)wave_sum_dpp(a12) * FLT_SCALE;
-                    A22 = (float)wave_sum_dpp(a22) * FLT_SCALE;
+                    wave_sum3_dpp(a11, a12, a22);
+                    A11 = (float)a11 * FLT_SCALE; A12 = (float)a12 * FLT_SCALE; A22 = (float)a22 * FLT_SCALE;
                 } else {
                     A11 = (float)wave_sum_split(a11) * FLT_SCALE; A12 = (float)wave_sum_split(a12) * FLT_SCALE;
                     A22 = (float)wave_sum_split(a22) * FLT_SCALE;
