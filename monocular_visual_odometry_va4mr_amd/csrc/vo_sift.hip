@@ -784,17 +784,21 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
                 pbin[slot] = bin;
                 pval[slot] = val;
             }
+            // slots nv .. (nv rounded up to 4) get bin -1, which no lane owns: the walk below
+            // needs no bounds test per pixel
+            if (lane >= nv && lane < ((nv + 3) & ~3)) pbin[lane] = -1;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // four pixels per step (entries past nv are masked to 0, which leaves th unchanged)
+            // four pixels per step; a pixel of another bin adds +0, which leaves th unchanged
+            // (th and every value are >= +0)
             for (int p0 = 0; p0 < nv; p0 += 4) {
                 const int4 bb = *reinterpret_cast<const int4*>(pbin + p0);
                 const float4 vv = *reinterpret_cast<const float4*>(pval + p0);
-                th += (p0 + 0 < nv && bb.x == lane) ? vv.x : 0.f;
-                th += (p0 + 1 < nv && bb.y == lane) ? vv.y : 0.f;
-                th += (p0 + 2 < nv && bb.z == lane) ? vv.z : 0.f;
-                th += (p0 + 3 < nv && bb.w == lane) ? vv.w : 0.f;
+                th += bb.x == lane ? vv.x : 0.f;
+                th += bb.y == lane ? vv.y : 0.f;
+                th += bb.z == lane ? vv.z : 0.f;
+                th += bb.w == lane ? vv.w : 0.f;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
