@@ -245,6 +245,13 @@ class Engine:
         launching thread right before (end=False) and after (end=True) each stage, with
         the torch stream that stage runs on (bench.py records HIP events there)."""
         frames = self._frames(frames)
+        la = getattr(self, "_la", None)
+        if la is not None:
+            # leaving lookahead mode: the pyramid built ahead may still be in flight into the
+            # buffer this step rebuilds; the state already points at (potential_frame, that buffer)
+            if la["ready"] is not None:
+                torch.cuda.current_stream(self.device).wait_event(la["ready"])
+            self._la = None
         self._step_launch(frames, self.prev, marks)
         self.prev = 1 - self.prev
 
@@ -264,18 +271,25 @@ class Engine:
         new frame's pyramid, which otherwise runs between two LK launches.  Three physical
         pyramid buffers rotate through the roles previous / current / next; the state's
         pyr[0] / pyr[1] are re-pointed before every step (prev = 0), so ``self.prev`` and the
-        state keep their usual meaning between steps.  Results are identical to step()."""
+        state keep their usual meaning between steps, and step() may follow (it leaves
+        lookahead mode).  Results are identical to step().  Not for captured graphs
+        (capture_step binds the buffers it saw at capture time)."""
         frames = self._frames(frames)
         frames_next = self._frames(frames_next)
         T = self.t
         if getattr(self, "_la", None) is None:
             for k in ("pyr", "der"):
-                T[k + "2"] = torch.zeros_like(T[k + "0"])
+                if k + "2" not in T:
+                    T[k + "2"] = torch.zeros_like(T[k + "0"])
             la = L.VoState()
             for name in L._STATE_FIELDS:
                 setattr(la, name, getattr(self.state, name))
-            # physical buffers in the roles (prev, cur, next); prev holds potential_frame
-            roles = [self.prev, 1 - self.prev, 2]
+            # physical buffers in the roles (prev, cur, next); prev holds potential_frame.  The
+            # state may point at any of the three (an earlier lookahead run rotated them)
+            phys = {T["pyr%d" % k].data_ptr(): k for k in range(3)}
+            p_prev = phys[getattr(self.state, "pyr%d" % self.prev)]
+            p_cur = phys[getattr(self.state, "pyr%d" % (1 - self.prev))]
+            roles = [p_prev, p_cur, 3 - p_prev - p_cur]
             self._la = {"state": la, "ps": C.byref(la), "roles": roles, "ready": None, "frames": None}
             # prologue: this frame's pyramid into the `cur` buffer, in stream order
             self._la_point(la, 0, roles[1])

@@ -37,20 +37,24 @@ def test_step_ahead_matches_step():
     dev = torch.device("cuda")
     frames = torch.from_numpy(seq).to(dev)
     engs = []
-    for ahead in (False, True):
+    # plain steps; lookahead throughout; lookahead, then plain steps, then lookahead again
+    for mode in ("step", "ahead", "mixed"):
         e = Engine(K, opts, fr.shape[2], fr.shape[1], batch=B, device=dev, ncap=4096, pcap=8192, fcap=64)
         e.bootstrap(frames[0], frames[1])
         for j in range(2, 2 + steps):
+            ahead = mode == "ahead" or (mode == "mixed" and not 5 <= j < 8)
             if ahead:
                 e.step_ahead(frames[j], frames[min(j + 1, 1 + steps)])
             else:
                 e.step(frames[j])
         torch.cuda.synchronize()
         engs.append(e)
-    a, b = _state(engs[0]), _state(engs[1])
+    a = _state(engs[0])
     assert int(a["nF"].min()) >= steps and (a["status"] == 0).all()
-    for k in a:
-        assert np.array_equal(a[k], b[k]), k
+    for e in engs[1:]:
+        b = _state(e)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
     # between steps pyr[prev] holds potential_frame's pyramid in both engines
     ref = engs[0].t["pyr%d" % engs[0].prev]
     la = engs[1]
