@@ -68,13 +68,6 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=100, help="CPU-baseline sample length")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--stagger", type=int, default=0, help="1: start the groups out of phase (see main)")
-    ap.add_argument("--lookahead", type=int, default=int(os.environ.get("VO_LOOKAHEAD", "0")),
-                    help="1: each step builds the next frame's pyramid (Engine.step_ahead; measured slower, see DESIGN); 0: its own")
-    ap.add_argument("--cu-reserve", type=int, default=int(os.environ.get("VO_CU_RESERVE", "0")),
-                    help="launch LK on a CU-masked stream per group that leaves this many CUs free "
-                         "for the other groups' latency-bound stages (0: off)")
-    ap.add_argument("--prio", default="none", choices=["none", "g0", "side"], help="HIP stream priorities of the groups")
     ap.add_argument("--cpu-threads", type=int, default=16, help="chains (processes) in the all-cores CPU leg (1: skip)")
     ap.add_argument("--cpu-mt-frames", type=int, default=30, help="steps per chain in the multi-thread CPU leg")
     ap.add_argument("--no-single", action="store_true", help="skip the single-chain latency / CPU leg "
@@ -82,10 +75,8 @@ def parse():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (see profiles/)")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
-    ap.add_argument("--no-match", action="store_true", help="skip the BF-matcher (MFMA) leg")
+    ap.add_argument("--no-match", action="store_true", help="skip the C3 / C5 legs (SIFT + BF matcher, C5 step)")
     ap.add_argument("--no-sequence", action="store_true", help="skip the whole-sequence (16-shard) leg")
-    ap.add_argument("--match-pairs", type=int, default=32, help="matcher leg: problems per launch")
-    ap.add_argument("--match-n", type=int, default=8192, help="matcher leg: descriptors per image")
     return ap.parse_args()
 
 
@@ -131,71 +122,81 @@ def gftt_bytes(eng, n_corners):
     return float(eng.B * eng.W * eng.H + 8 * n_corners)
 
 
-def matcher_leg(device, pairs, n, iters=10):
-    """BF kNN (k=2) on MFMA, SURVEY.md §8d / BASELINE config C5 ("SIFT capped at the best 8192 +
-    BF 8192^2"): `pairs` image pairs of n SIFT-like descriptors per vo_bf_knn2_batch launch,
-    timed with HIP events; 2*n*n*128 FLOP per pair against the dense bf16 MFMA peak."""
-    from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch
-    rng = np.random.default_rng(7)
+def sift_bytes(sift) -> float:
+    """SURVEY.md §8d SIFT algorithmic bytes per image: 2 x 11 x 4 B per scale-space pixel (6
+    Gaussians + 5 DoG layers, fp32, each written once and read once) over the octaves."""
+    sb = sift.sb
+    spx = sum(int(sb.oct_w[o]) * int(sb.oct_h[o]) for o in range(sb.n_oct))
+    return 88.0 * spx
 
-    def sift_like():
-        v = rng.gamma(0.6, 1.0, (pairs, n, 128))
-        v *= 512.0 / np.linalg.norm(v, axis=2, keepdims=True)
-        v = np.minimum(v, 0.2 * 512)
-        v *= 512.0 / np.maximum(np.linalg.norm(v, axis=2, keepdims=True), 1e-9)
-        return torch.from_numpy(np.clip(np.rint(v), 0, 255).astype(np.float32)).to(device)
 
-    q, t = sift_like(), sift_like()
-    cnt = torch.full((pairs,), n, dtype=torch.int32, device=device)
-    for _ in range(2):
-        bf_knn2_batch(q, cnt, t, cnt)
+def sift_match_leg(device, preset, seed, n_frames, nfeatures=0, iters=2):
+    """Detect + describe `n_frames` consecutive synthetic frames in ONE vo_sift_batch launch
+    sequence, then match the n_frames - 1 consecutive pairs in ONE vo_bf_knn2_batch launch
+    (BFMatcher.knnMatch k=2 on MFMA), each timed with HIP events on the current stream.
+    Rooflines: SIFT against HBM (sift_bytes per image), BF against the dense bf16 MFMA peak
+    (2 * nq * nt * 128 FLOP per pair on the real descriptor counts)."""
+    from monocular_visual_odometry_va4mr_amd.features import Sift, bf_knn2_batch
+    rend = Renderer(preset, seed=seed, device=device)
+    Rs, cs = poses(n_frames, rend.p)
+    frames = rend.render_batch(list(range(n_frames)), Rs, cs)
+    sift = Sift(rend.W, rend.H, device, batch=n_frames, nfeatures=nfeatures)
+
+    def run():
+        kp, desc, n = sift.run_batch(frames)
+        e1.record()
+        out = bf_knn2_batch(desc[:-1], n[:-1], desc[1:], n[1:])
+        return n, out
+
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    run()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    if sift.overflowed(n_frames):
+        raise RuntimeError("SIFT capacity exceeded")
+    t_sift = t_bf = 0.0
     for _ in range(iters):
-        bf_knn2_batch(q, cnt, t, cnt)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    tf = 2.0 * n * n * 128 * pairs / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": "vo_bf_knn2_batch", "achieved": round(tf, 2), "peak": MFMA_PEAK_TF,
-            "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TF, 4), "pairs_per_s": round(pairs / (ms * 1e-3), 1),
-            "ms_per_launch": round(ms, 4), "config": f"C5 BF {n}x{n} descriptors x {pairs} pairs per launch",
-            "flop_per_launch": 2.0 * n * n * 128 * pairs}
+        e0.record()
+        n, _ = run()
+        e2.record()
+        torch.cuda.synchronize()
+        t_sift += e0.elapsed_time(e1) / iters
+        t_bf += e1.elapsed_time(e2) / iters
+    nn = n.to(torch.float64).cpu().numpy()
+    pairs = n_frames - 1
+    flop = float(2.0 * 128 * (nn[:-1] * nn[1:]).sum())
+    tf = flop / (t_bf * 1e-3) / 1e12
+    sb = sift_bytes(sift) * n_frames
+    gbs = sb / (t_sift * 1e-3) / 1e9
+    return {"frames": n_frames, "pairs": pairs, "keypoints_mean": round(float(nn.mean()), 1),
+            "sift_ms_per_image": round(t_sift / n_frames, 4), "bf_ms_per_pair": round(t_bf / pairs, 4),
+            "pairs_per_s": round(pairs / ((t_sift * pairs / n_frames + t_bf) * 1e-3), 1),
+            "sift_roofline": {"bound": "hbm", "kernel": "vo_sift_batch", "achieved": round(gbs, 2),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+                              "algorithmic_bytes_per_image": sift_bytes(sift)},
+            "bf_roofline": {"bound": "mfma", "kernel": "vo_bf_knn2_batch", "achieved": round(tf, 2),
+                            "peak": MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TF, 4),
+                            "flop_per_launch": flop}}
 
 
 def c3_leg(device, n_pairs=16, iters=2):
     """BASELINE config C3 ("Malaga 1024x768, stresses SIFT + BF-match MFMA path"): n_pairs + 1
-    consecutive synthetic 1024x768 frames; SIFT detectAndCompute on every frame (vo_sift), then
-    one batched 2-NN over all consecutive pairs (vo_bf_knn2_batch), timed with HIP events.
+    consecutive synthetic 1024x768 frames, SIFT detectAndCompute batched over all of them
+    (vo_sift_batch) and one batched 2-NN over the consecutive pairs (vo_bf_knn2_batch).
     pairs/s = one new frame's SIFT + one match per pair."""
-    from monocular_visual_odometry_va4mr_amd.features import Sift, bf_knn2_batch
-    rend = Renderer("malaga1024", seed=2, device=device)
-    Rs, cs = poses(n_pairs + 1, rend.p)
-    frames = rend.render_batch(list(range(n_pairs + 1)), Rs, cs)
-    sift = Sift(rend.W, rend.H, device)
-    D = torch.zeros((n_pairs + 1, sift.kp_cap, 128), dtype=torch.float32, device=device)
-    N = torch.zeros(n_pairs + 1, dtype=torch.int32, device=device)
+    r = sift_match_leg(device, "malaga1024", 2, n_pairs + 1, nfeatures=0, iters=iters)
+    r["config"] = (f"C3 malaga1024 synthetic, {n_pairs} consecutive pairs: SIFT batched over "
+                   f"{n_pairs + 1} frames + batched BF 2-NN")
+    return r
 
-    def run():
-        for i in range(n_pairs + 1):
-            _, desc, n = sift.run(frames[i])
-            D[i].copy_(desc)
-            N[i:i + 1].copy_(n)
-        return bf_knn2_batch(D[:-1], N[:-1], D[1:], N[1:])
 
-    run()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    return {"config": f"C3 malaga1024 synthetic, {n_pairs} consecutive pairs: SIFT per frame + batched BF 2-NN",
-            "pairs_per_s": round(n_pairs / (ms * 1e-3), 1), "ms_per_pair": round(ms / n_pairs, 3),
-            "keypoints_mean": round(float(N.float().mean()), 1)}
+def c5_sift_leg(device, n_pairs=16, iters=2):
+    """BASELINE config C5's SIFT half ("SIFT capped at the best 8192 + BF 8192^2"): n_pairs + 1
+    consecutive synthetic 1920x1080 frames, SIFT_create(nfeatures=8192) batched over all of
+    them, the consecutive 8192 x 8192 pairs matched in one launch."""
+    r = sift_match_leg(device, "hd1080", 3, n_pairs + 1, nfeatures=8192, iters=iters)
+    r["config"] = (f"C5 hd1080 synthetic, {n_pairs} consecutive pairs: SIFT capped at 8192 batched over "
+                   f"{n_pairs + 1} frames + batched BF 8192x8192 2-NN")
+    return r
 
 
 def c5_leg(device, chains=256, steps=6, warmup=2, groups=2):
@@ -287,6 +288,8 @@ def sequence_leg(device, seed, rank, world, n_shards=16):
     return {"config": f"C2 whole sequence: {SEQ_LEN} frames as {res['shards']} overlapping shards on {world} GPU(s), "
                       "bootstrap + every step timed, poses gathered + Sim(3)-stitched after",
             "frames_per_s": res["sequence_frames_per_s"], "wall_s": res["wall_s"], "shards_ok": res["shards_ok"],
+            "gather_ms": res["gather_ms"], "stitch_ms": res["stitch_ms"],
+            "frames_per_s_incl_gather_stitch": res["job_frames_per_s"],
             "failed_shards": res["failed_shards"], "vs_reference": res.get("vs_reference"),
             "stitched_frames": st.get("frames"), "coverage_breaks": st.get("coverage_breaks"),
             "stitched_ate_rel_vs_gt": st.get("ate_rel")}
@@ -422,14 +425,7 @@ def main():
     for g in range(G):
         engines.append(Engine(Kmat, opts, Wd, H, batch=bounds[g + 1] - bounds[g], device=device,
                               ncap=16384, pcap=16384, fcap=n_after + 16))
-        # --prio g0: group 0's streams at high priority, so its latency-bound stages are never
-        # queued behind another group's bulk launches (the other groups fill the idle CUs)
-        hi = args.prio == "g0" and g == 0 and G > 1
-        engines[-1].side_priority = -1 if (hi or args.prio == "side") else 0
-        streams.append(torch.cuda.Stream(device, priority=-1 if hi else 0) if G > 1 else torch.cuda.current_stream(device))
-        if args.cu_reserve > 0 and G > 1:
-            from monocular_visual_odometry_va4mr_amd.engine import cu_masked_stream
-            engines[-1].bulk_stream, _h = cu_masked_stream(device, args.cu_reserve)
+        streams.append(torch.cuda.Stream(device) if G > 1 else torch.cuda.current_stream(device))
     eng = engines[0]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -439,41 +435,13 @@ def main():
     torch.cuda.synchronize()
     boot_s = time.perf_counter() - t0
 
-    last = frames.shape[0] - 1
-
     def step_all(j, marks=None):
         for g, e in enumerate(engines):
             with torch.cuda.stream(streams[g]):
-                mk = marks if g == 0 else None
-                if args.lookahead:
-                    # one frame of pyramid lookahead: step j also builds frame j+1's pyramid
-                    # (the last step rebuilds its own frame's: the same work per step)
-                    e.step_ahead(frames[j, bounds[g]:bounds[g + 1]],
-                                 frames[min(j + 1, last), bounds[g]:bounds[g + 1]], marks=mk)
-                else:
-                    e.step(frames[j, bounds[g]:bounds[g + 1]], marks=mk)
+                e.step(frames[j, bounds[g]:bounds[g + 1]], marks=marks if g == 0 else None)
 
-    # --stagger: group g starts its first step only when group g-1's first `track` stage has
-    # ended, so the groups run out of phase: one group's latency-bound stages (PnP, select,
-    # triangulate) overlap another group's bulk stages (pyramid, LK, eig3) instead of all
-    # groups reaching their latency-bound stages together
     for i in range(W_steps):
-        if i == 0 and args.stagger and G > 1:
-            tr = Engine.STAGES.index("track")
-            prev_ev = None
-            for g, e in enumerate(engines):
-                if prev_ev is not None:
-                    streams[g].wait_event(prev_ev)
-                ev_g = torch.cuda.Event()
-
-                def mark(si, end, strm, ev_g=ev_g):
-                    if si == tr and end:
-                        ev_g.record(strm)
-                with torch.cuda.stream(streams[g]):
-                    e.step(frames[2 + i, bounds[g]:bounds[g + 1]], marks=mark)
-                prev_ev = ev_g
-        else:
-            step_all(2 + i)
+        step_all(2 + i)
     torch.cuda.synchronize()
 
     nst = len(Engine.STAGES)
@@ -599,7 +567,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": "C2 kitti seq00-length synthetic 1241x376, per-frame continuous_operation",
                    "width": Wd, "height": H, "chains_per_gpu": B, "frames_per_step": world * B,
-                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "cu_reserve": args.cu_reserve, "pyramid_lookahead": args.lookahead, "seq_len": SEQ_LEN,
+                   "parallelism": f"shards{world}x{B}", "streams_per_gpu": G, "seq_len": SEQ_LEN,
                    "seed": args.seed},
         "roofline": roof,
         "roofline_valu": roof_valu,
@@ -651,12 +619,16 @@ def main():
     else:
         out["cpu_baseline"] = None
     if world == 1 and not args.no_match:
-        out["roofline_matcher"] = matcher_leg(device, args.match_pairs, args.match_n)
-        for key, leg in (("c3_sift_match", c3_leg), ("c5_hd1080", c5_leg)):
+        for key, leg in (("c3_sift_match", c3_leg), ("c5_sift_match", c5_sift_leg), ("c5_hd1080", c5_leg)):
             try:                      # secondary configurations never cost the headline line
                 out[key] = leg(device)
+                torch.cuda.empty_cache()
             except Exception as exc:  # noqa: BLE001
                 out[key] = {"error": f"{type(exc).__name__}: {exc}"}
+        # the matcher's MFMA roofline on real descriptors: C5's capped SIFT output
+        c5s = out.get("c5_sift_match") or {}
+        if "bf_roofline" in c5s:
+            out["roofline_matcher"] = dict(c5s["bf_roofline"], config=c5s["config"])
     print(json.dumps(out))
     if args.stages:
         print(json.dumps({"stages_ms": stage, "bytes": bytes_by}), file=sys.stderr)

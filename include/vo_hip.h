@@ -126,10 +126,6 @@ typedef struct vo_state {
 const char* vo_version(void);
 int vo_device_arch(char* buf, int len);          /* gcnArchName of the current device */
 int vo_device_cus(void);                          /* compute units of the current device (or < 0) */
-/* Runtime helpers (no reference counterpart): a HIP stream restricted to the CUs whose bits
- * are set in mask[nwords] (bit i of word i/32 = CU i), and its release. */
-int vo_stream_create_cumask(int nwords, const uint32_t* mask, vo_stream_t* out);
-int vo_stream_destroy(vo_stream_t s);
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 
@@ -218,13 +214,17 @@ typedef struct vo_sift_buf {
     float* kp_out;                /* sorted, deduplicated keypoints [kp_cap][6]         */
     float* desc;                  /* descriptors [kp_cap][128] (integer-valued floats)  */
     float* hist;                  /* descriptor histogram scratch [kp_cap][360]         */
-    int32_t cand_cap, kp_cap;
+    int32_t cand_cap, kp_cap;     /* kp_cap <= 32768 (raw keypoints sorted in LDS)       */
+    int32_t nfeatures;            /* SIFT_create(nfeatures): > 0 applies retainBest      */
 } vo_sift_buf;
 
-/* Fill the geometry of `sb` for a W x H image (host only, no device work). */
+/* Fill the geometry of `sb` for a W x H image (host only, no device work); resets
+ * nfeatures to 0 (no cap). */
 int vo_sift_plan(vo_sift_buf* sb, int W, int H);
 
-/* cv2.SIFT_create().detectAndCompute(img, None) (:35,226-227) for one image. */
+/* cv2.SIFT_create().detectAndCompute(img, None) (:35,226-227) for one image;
+ * sb->nfeatures > 0 is SIFT_create(nfeatures) (BASELINE C5's capped SIFT): the keypoints are
+ * cut by KeyPointsFilter::retainBest in libstdc++'s nth_element/partition order. */
 int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream);
 
 /* detectAndCompute for B images per launch sequence (the bootstrap of B chains, :226-227

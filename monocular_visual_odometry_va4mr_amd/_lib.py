@@ -92,7 +92,7 @@ class VoSiftBuf(C.Structure):
         ("gauss_floats", i64), ("dog_floats", i64), ("tmp_floats", i64),
         ("gauss", vp), ("dog", vp), ("tmp", vp), ("consts", vp), ("counters", vp), ("cand", vp),
         ("kp", vp), ("kp_out", vp), ("desc", vp), ("hist", vp),
-        ("cand_cap", i32), ("kp_cap", i32),
+        ("cand_cap", i32), ("kp_cap", i32), ("nfeatures", i32),
     ]
 
 
@@ -128,8 +128,6 @@ def _declare(L):
         "vo_version": ([], C.c_char_p),
         "vo_device_arch": ([C.c_char_p, C.c_int], C.c_int),
         "vo_device_cus": ([], C.c_int),
-        "vo_stream_create_cumask": ([C.c_int, P, P], C.c_int),
-        "vo_stream_destroy": ([P], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),

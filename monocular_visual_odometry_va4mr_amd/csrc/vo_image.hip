@@ -996,311 +996,6 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
     LKPROF_SET(1, wall_clock64());
 }
 
-// ---------------------------------------------------------------------------------------
-// k_lk_q: the same calcOpticalFlowPyrLK arithmetic as k_lk_w<15,15> (bit-exact with the CPU
-// restatement) with FOUR points per wave.  Lane = (group g = lane / 16, window column
-// c = lane % 16): a group of 16 lanes (one DPP row) carries one point, each lane one window
-// column and its 15 rows in registers (lane 15 holds the extra bilinear column and
-// contributes zeros).  The per-point scalar work (weights, the 2x2 solve, convergence
-// tests) is shared by the four groups, the window sums are 16-lane DPP row reductions.
-//
-// Groups advance independently through a small state machine -- SETUP (stage the level's
-// I / dI window and the structure tensor), ITER (one solver iteration), ERR (the level-0
-// error) -- and pull their next point from the block's chunk list when done, so a slow
-// point does not stall the other three.  The SETUP code runs when two groups need it (or
-// one has waited three passes, or nothing else is running), which amortises it over
-// several groups.
-//
-// Window rows are read straight from the pyramids with buffer loads: every level has the
-// pitch of level 0, so row r of any level is the scalar offset r * pitch (no per-row VALU
-// address arithmetic) and the derivatives come from separate dx / dy planes as sign-
-// extending 16-bit loads.  Buffer loads are bounds-checked by the resource (a stray
-// offset reads zeros instead of faulting).
-#define LKQ_CH 32          // points per chunk (block work unit)
-#define LKQ_WW 15
-#define LKQ_WH 15
-
-enum { LKQ_IDLE = 0, LKQ_SETUP = 1, LKQ_ITER = 2, LKQ_ERR = 3 };
-
-VO_DEV int dpp_row_next(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xF, 0xF, false); }  // lane c <- c+1 (row)
-VO_DEV int row_sum16(int x)
-{
-    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    x += __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // row_ror:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
-    return x;                                                         // every lane of the row
-}
-VO_DEV int64_t row_sum16_split(int p)
-{
-    const int lo = p & 0xFFFF, hi = p >> 16;
-    return (int64_t)row_sum16(hi) * 65536 + (int64_t)row_sum16(lo);
-}
-
-__global__ void __launch_bounds__(64) k_lk_q(LKParams P, int B, int nb)
-{
-    constexpr int WW = LKQ_WW, WH = LKQ_WH;
-    __shared__ int lv_cols[VO_MAX_LEVELS], lv_rows[VO_MAX_LEVELS], lv_off[VO_MAX_LEVELS];
-    const int b = blockIdx.x / nb, pb = blockIdx.x - b * nb;
-    if (b >= B) return;
-    if (P.chain_status && P.chain_status[b] != 0) return;
-    const int n0 = P.n0 ? P.n0[b] : 0;
-    int n1 = P.n1 ? P.n1[b] : 0;
-    if (n1 <= P.seg1_min) n1 = 0;
-    const int ntot = n0 + n1;
-    if (pb * LKQ_CH >= ntot) return;
-    const int lane = lane_id();
-    if (lane < VO_MAX_LEVELS) {
-        lv_cols[lane] = P.lw[lane];
-        lv_rows[lane] = P.lh[lane];
-        lv_off[lane] = (int)P.loff[lane];
-    }
-    wave_lds_sync();
-    const int g = lane >> 4, c = lane & 15;
-    const int pitch = P.lpitch[0];
-    const __amdgpu_buffer_rsrc_t rI = lkq_rsrc(P.prev + (int64_t)b * P.pstride, P.pstride);
-    const __amdgpu_buffer_rsrc_t rJ = lkq_rsrc(P.next + (int64_t)b * P.pstride, P.pstride);
-    const __amdgpu_buffer_rsrc_t rX = lkq_rsrc(P.der + (int64_t)b * P.dstride, 2 * P.dplane);
-    const __amdgpu_buffer_rsrc_t rY = lkq_rsrc(P.der + (int64_t)b * P.dstride + P.dplane, 2 * P.dplane);
-    const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
-    const float FLT_SCALE = 1.f / (1 << 20);
-
-    // group state (uniform across the 16 lanes of a group)
-    int phase = LKQ_IDLE, level = 0, wait = 0, it = 0, status = 1;
-    int pidx = -1;
-    bool gdone = false;
-    int64_t oidx = 0;
-    float ptx = 0.f, pty = 0.f, ox = 0.f, oy = 0.f, nx = 0.f, ny = 0.f, pdx = 0.f, pdy = 0.f;
-    float A11 = 0.f, A12 = 0.f, A22 = 0.f, Dinv = 0.f, errv = 0.f;
-    int cols = 0, rows = 0, loff = 0;
-    // window column c, rows 0..14: I (x32), Ix, Iy
-    int ival[WH], ixv[WH], iyv[WH];
-#pragma unroll
-    for (int r = 0; r < WH; ++r) { ival[r] = 0; ixv[r] = 0; iyv[r] = 0; }
-    int kq = 0;                                  // wave-uniform: next point of this block
-
-    while (true) {
-        // ------------------------------------------------ assignment of new points
-        {
-            const bool want = pidx < 0 && !gdone;
-            const uint64_t wm = __ballot(want && c == 0);
-            if (wm) {
-                const int rank = __popcll(wm & ((1ull << (16 * g)) - 1ull));
-                if (want) {
-                    const int k = kq + rank;
-                    const int p = (pb + nb * (k / LKQ_CH)) * LKQ_CH + (k % LKQ_CH);
-                    if (p < ntot) {
-                        const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2)
-                                                    : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
-                        ptx = src[0];
-                        pty = src[1];
-                        pidx = p;
-                        oidx = (int64_t)b * P.ocap + p;
-                        level = P.L;
-                        status = 1;
-                        errv = 0.f;
-                        phase = LKQ_SETUP;
-                        wait = 0;
-                    } else {
-                        gdone = true;
-                    }
-                }
-                kq += __popcll(wm);
-            }
-        }
-        if (__ballot(pidx >= 0) == 0) break;
-        bool ldone = false;                      // the group's current level finished
-        bool fin = false;                        // the group's point finished
-        // ------------------------------------------------ SETUP: I / dI window + tensor
-        {
-            const uint64_t need = __ballot(phase == LKQ_SETUP && c == 0);
-            const uint64_t busy = __ballot((phase == LKQ_ITER || phase == LKQ_ERR) && c == 0);
-            const uint64_t late = __ballot(phase == LKQ_SETUP && wait >= 3 && c == 0);
-            const bool run = need && (__popcll(need) >= 2 || !busy || late);
-            if (!run) {
-                if (phase == LKQ_SETUP) ++wait;
-            } else if (phase == LKQ_SETUP) {
-                cols = lv_cols[level];
-                rows = lv_rows[level];
-                loff = lv_off[level];
-                const float sc = (float)(1. / (1 << level));
-                float px = ptx * sc, py = pty * sc;
-                if (level == P.L) { ox = px; oy = py; }
-                px -= hx;
-                py -= hy;
-                const int ipx = (int)floorf(px), ipy = (int)floorf(py);
-                if (ipx < -WW || ipx >= cols || ipy < -WH || ipy >= rows) {
-                    if (level == 0) { status = 0; errv = 0.f; }
-                    ldone = true;
-                } else {
-                    const float a = px - ipx, bb = py - ipy;
-                    const int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
-                    const int iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
-                    const int iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
-                    const int iw11 = (1 << 14) - iw00 - iw01 - iw10;
-                    const int vo = loff + (ipy + VO_BORDER) * pitch + ipx + VO_BORDER + c;
-                    int Ir[WH + 1], Xr[WH + 1], Yr[WH + 1];
-#pragma unroll
-                    for (int r = 0; r <= WH; ++r) {
-                        Ir[r] = __builtin_amdgcn_raw_buffer_load_b8(rI, vo, r * pitch, 0);
-                        Xr[r] = (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rX, 2 * vo, 2 * r * pitch, 0);
-                        Yr[r] = (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rY, 2 * vo, 2 * r * pitch, 0);
-                    }
-                    int a11 = 0, a12 = 0, a22 = 0;
-                    int In0 = dpp_row_next(Ir[0]), Xn0 = dpp_row_next(Xr[0]), Yn0 = dpp_row_next(Yr[0]);
-#pragma unroll
-                    for (int r = 0; r < WH; ++r) {
-                        const int In1 = dpp_row_next(Ir[r + 1]), Xn1 = dpp_row_next(Xr[r + 1]), Yn1 = dpp_row_next(Yr[r + 1]);
-                        const int v = DESCALE(__mul24(Ir[r], iw00) + __mul24(In0, iw01) + __mul24(Ir[r + 1], iw10) +
-                                              __mul24(In1, iw11), 9);
-                        const int gx = DESCALE(__mul24(Xr[r], iw00) + __mul24(Xn0, iw01) + __mul24(Xr[r + 1], iw10) +
-                                               __mul24(Xn1, iw11), 14);
-                        const int gy = DESCALE(__mul24(Yr[r], iw00) + __mul24(Yn0, iw01) + __mul24(Yr[r + 1], iw10) +
-                                               __mul24(Yn1, iw11), 14);
-                        ival[r] = c < WW ? v : 0;
-                        ixv[r] = c < WW ? gx : 0;
-                        iyv[r] = c < WW ? gy : 0;
-                        a11 += __mul24(ixv[r], ixv[r]);
-                        a12 += __mul24(ixv[r], iyv[r]);
-                        a22 += __mul24(iyv[r], iyv[r]);
-                        In0 = In1; Xn0 = Xn1; Yn0 = Yn1;
-                    }
-                    const int64_t iA11 = row_sum16_split(a11), iA12 = row_sum16_split(a12), iA22 = row_sum16_split(a22);
-                    A11 = (float)iA11 * FLT_SCALE;
-                    A12 = (float)iA12 * FLT_SCALE;
-                    A22 = (float)iA22 * FLT_SCALE;
-                    float D = A11 * A22 - A12 * A12;
-                    const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
-                                         (float)(2 * WW * WH);
-                    if (minEig < P.min_eig || D < FLT_EPSILON) {
-                        if (level == 0) status = 0;
-                        ldone = true;
-                    } else {
-                        Dinv = 1.f / D;
-                        nx = ox - hx;
-                        ny = oy - hy;
-                        pdx = pdy = 0.f;
-                        it = 0;
-                        phase = LKQ_ITER;
-                        if (P.max_count <= 0) ldone = true;
-                    }
-                }
-            }
-        }
-        // ------------------------------------------------ ITER / ERR: one J pass
-        {
-            const bool jg = (phase == LKQ_ITER && !ldone) || phase == LKQ_ERR;
-            const uint64_t jm = __ballot(jg);
-            if (jm) {
-                const bool errp = phase == LKQ_ERR;
-                const float fx = errp ? ox - hx : nx, fy = errp ? oy - hy : ny;
-                const int inx = (int)floorf(fx), iny = (int)floorf(fy);
-                const bool outside = inx < -WW || inx >= cols || iny < -WH || iny >= rows;
-                if (jg && outside) {
-                    if (level == 0) status = 0;
-                    if (errp) fin = true; else ldone = true;
-                }
-                const bool go = jg && !outside;
-                const uint64_t gm = __ballot(go);
-                if (gm) {
-                    const bool any_err = __ballot(go && errp) != 0;
-                    int w00 = 0, w01 = 0, w10 = 0, w11 = 0;
-                    {
-                        const float a = fx - inx, bb = fy - iny;
-                        w00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
-                        w01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
-                        w10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
-                        w11 = (1 << 14) - w00 - w01 - w10;
-                    }
-                    // iw11 can be -1: dot with w11 + 1 and subtract the tap once
-                    const int neg = w11 < 0;
-                    const bool any_neg = __ballot(go && neg) != 0;
-                    const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
-                    const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
-                    const uint32_t negm = neg ? 0xFFFFFFFFu : 0u;
-                    int b1 = 0, b2 = 0, es = 0;
-                    if (go) {
-                        const int vo = loff + (iny + VO_BORDER) * pitch + inx + VO_BORDER + c;
-                        uint32_t Jr[WH + 1];
-#pragma unroll
-                        for (int r = 0; r <= WH; ++r) Jr[r] = __builtin_amdgcn_raw_buffer_load_b8(rJ, vo, r * pitch, 0);
-                        uint32_t pr0 = Jr[0] | ((uint32_t)dpp_row_next((int)Jr[0]) << 8);
-#pragma unroll
-                        for (int r = 0; r < WH; ++r) {
-                            const uint32_t pr1 = Jr[r + 1] | ((uint32_t)dpp_row_next((int)Jr[r + 1]) << 8);
-                            const uint32_t q = pr0 | (pr1 << 16);
-                            pr0 = pr1;
-                            uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
-                                           __builtin_amdgcn_udot4(q, wlo, 256u, false);
-                            if (any_neg) sum -= (q >> 24) & negm;
-                            const int diff = (int)(sum >> 9) - ival[r];
-                            b1 += __mul24(diff, ixv[r]);      // |diff| <= 8160, |grad| <= 4080
-                            b2 += __mul24(diff, iyv[r]);
-                            if (any_err) es += c < WW ? (diff < 0 ? -diff : diff) : 0;
-                        }
-                    }
-                    // 16-lane sums (exact: split when a lane's partial could overflow the row)
-                    const bool wide = __ballot((uint32_t)(b1 + (1 << 26)) >= (1u << 27) ||
-                                               (uint32_t)(b2 + (1 << 26)) >= (1u << 27)) != 0;
-                    int64_t s1, s2;
-                    if (!wide) { s1 = row_sum16(b1); s2 = row_sum16(b2); }
-                    else { s1 = row_sum16_split(b1); s2 = row_sum16_split(b2); }
-                    int esum = 0;
-                    if (any_err) esum = row_sum16(es);
-                    if (go && errp) {
-                        errv = (float)esum / (float)(32 * WW * WH);
-                        fin = true;
-                    } else if (go) {
-                        const float fb1 = (float)s1 * FLT_SCALE;
-                        const float fb2 = (float)s2 * FLT_SCALE;
-                        const float ddx = (A12 * fb2 - A22 * fb1) * Dinv;
-                        const float ddy = (A12 * fb1 - A11 * fb2) * Dinv;
-                        nx += ddx;
-                        ny += ddy;
-                        ox = nx + hx;
-                        oy = ny + hy;
-                        if ((double)ddx * ddx + (double)ddy * ddy <= P.eps2) {
-                            ldone = true;
-                        } else if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
-                            ox -= ddx * 0.5f;
-                            oy -= ddy * 0.5f;
-                            ldone = true;
-                        }
-                        pdx = ddx;
-                        pdy = ddy;
-                        ++it;
-                        if (it >= P.max_count) ldone = true;
-                    }
-                }
-            }
-        }
-        // ------------------------------------------------ transitions
-        if (ldone) {
-            if (level > 0) {
-                --level;
-                ox *= 2.f;
-                oy *= 2.f;
-                phase = LKQ_SETUP;
-                wait = 0;
-            } else if (status) {
-                phase = LKQ_ERR;
-            } else {
-                fin = true;
-            }
-        }
-        if (fin) {
-            if (c == 0) {
-                P.out[2 * oidx] = ox;
-                P.out[2 * oidx + 1] = oy;
-                P.st[oidx] = (uint8_t)status;
-                if (P.err) P.err[oidx] = errv;
-            }
-            pidx = -1;
-            phase = LKQ_IDLE;
-        }
-    }
-}
-
 // ---------------------------------------------------- tracking compaction (:282-290)
 __global__ void __launch_bounds__(256) k_track_compact(vo_dims d, vo_state s)
 {
@@ -2309,23 +2004,8 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     // 0 in registers) unless VO_LK_FUSED=0: a level's launch lasts as long as its slowest
     // point (up to max_count iterations), so separate launches pay that tail once per level.
     static const int fused_env = [] { const char* e = getenv("VO_LK_FUSED"); return e ? atoi(e) : 1; }();
-    // four points per wave (k_lk_q, VO_LK_QUAD=1) when every level shares one pitch (the
-    // engine's layout); opt-in: at 162 VGPRs it holds 3 waves per SIMD and measured slower
-    static const int q_env = [] { const char* e = getenv("VO_LK_QUAD"); return e ? atoi(e) : 0; }();
-    static const int qnb_env = [] { const char* e = getenv("VO_LK_QNB"); return e ? atoi(e) : 64; }();
-    bool one_pitch = true;
-    for (int l = 1; l <= L; ++l) one_pitch = one_pitch && P.lpitch[l] == P.lpitch[0];
-    if (P.win_w == LKQ_WW && P.win_h == LKQ_WH && one_pitch && q_env && fused_env) {
-        const int nbq = qnb_env > 0 ? qnb_env : 64;      // blocks per chain (grid-stride over chunks)
-        hipLaunchKernelGGL(k_lk_q, dim3(B * nbq), dim3(64), 0, st, P, B, nbq);
-        return hip_ok() ? VO_OK : VO_EHIP;
-    }
-    static const int wpb_env = [] { const char* e = getenv("VO_LK_WPB"); return e ? atoi(e) : 1; }();
     if (staged15 && fused_env) {
-        if (wpb_env == 4 && nblk % 4 == 0)
-            hipLaunchKernelGGL((k_lk_w<15, 15, 4>), dim3(nblk / 4), dim3(256), 0, st, P, L, 0, B, nb, xcd_env);
-        else
-            hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
+        hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {

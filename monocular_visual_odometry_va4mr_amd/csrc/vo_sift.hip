@@ -863,11 +863,13 @@ VO_DEV bool kp_less(const float* a, const float* b)
     return false;
 }
 
-#define SORT_N 16384
+// keypoint indices as 16-bit LDS entries: 32,768 raw keypoints per image in 64 KB
+#define SORT_N 32768
+#define SORT_PAD 0xFFFFu
 __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
-    __shared__ int idx[SORT_N];
+    __shared__ uint16_t idx[SORT_N];
     __shared__ int lds[16];
     const int tid = threadIdx.x;
     const int n = min(im.counters[1], sb.kp_cap);
@@ -875,7 +877,7 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
     const int nn = n < SORT_N ? n : SORT_N;
     int P = 1;
     while (P < nn) P <<= 1;
-    for (int i = tid; i < P; i += blockDim.x) idx[i] = i < nn ? i : -1;
+    for (int i = tid; i < P; i += blockDim.x) idx[i] = i < nn ? (uint16_t)i : (uint16_t)SORT_PAD;
     __syncthreads();
     for (int size = 2; size <= P; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -883,13 +885,13 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
                 const int lo = 2 * i - (i & (stride - 1));
                 const int hi = lo + stride;
                 const bool asc = ((lo & size) == 0);
-                const int a = idx[lo], c = idx[hi];
-                // "a > c" in kp_less order, padding (-1) sorts last
+                const unsigned a = idx[lo], c = idx[hi];
+                // "a > c" in kp_less order, padding sorts last
                 bool gt;
-                if (a < 0) gt = c >= 0;
-                else if (c < 0) gt = false;
+                if (a == SORT_PAD) gt = c != SORT_PAD;
+                else if (c == SORT_PAD) gt = false;
                 else gt = kp_less(im.kp + 8 * (int64_t)c, im.kp + 8 * (int64_t)a);
-                if (gt == asc) { idx[lo] = c; idx[hi] = a; }
+                if (gt == asc) { idx[lo] = (uint16_t)c; idx[hi] = (uint16_t)a; }
             }
             __syncthreads();
         }
@@ -919,6 +921,207 @@ __global__ void __launch_bounds__(1024) k_sift_sort_dedupe(vo_sift_buf sb)
         out += tot;
     }
     if (tid == 0) im.counters[2] = out;
+}
+
+// ------------------------------------------------------- KeyPointsFilter::retainBest
+// SIFT_create(nfeatures) (BASELINE C5: "SIFT capped at the best 8192"): after
+// removeDuplicatedSorted, retainBest(keypoints, nfeatures) (features2d/src/keypoint.cpp) =
+// std::nth_element(KeypointResponseGreater) on the n-th position, then std::partition of the
+// rest by response >= that boundary response, then resize.  The kept keypoints stay in the
+// order libstdc++'s algorithms leave them (the BF query order downstream); the oracle restates
+// them step for step (oracle/vo_oracle_sift.c) and tests/test_retain_best.py pins that against
+// the real std::nth_element.  The firstOctave scaling in k_sift_sort_dedupe does not touch the
+// response, so selecting after it is the same.
+//
+// Block-parallel form of every Hoare round of __introselect: the scan pointer i stops at the
+// k-th "left stopper" (!(r > pivot)) and j at the k-th "right stopper" (!(pivot > r)) of the
+// range in the ORIGINAL order, as long as they have not crossed (the elements a swap moves
+// are stoppers for the other pointer, so nothing in between changes).  A round therefore
+// compacts both stopper lists with ordered block scans, counts K = #{k : L_k < R_k} (monotone),
+// swaps the K pairs at once, and cuts at min(L_K, R_{K-1}).  std::partition's bidirectional
+// loop is the same pairing with the stoppers !(r >= amb) / (r >= amb).  The median-of-3 pivot
+// move, the final insertion sort of <= 3 records and the depth-limit __heap_select fallback
+// (adversarial inputs only) run on one thread, like libstdc++.  Records (response bits, index)
+// live in the image's candidate buffer, free after k_sift_refine.
+#define RB_T 1024
+VO_DEV bool rb_gt(int2 a, int2 b) { return __int_as_float(a.x) > __int_as_float(b.x); }
+VO_DEV void rb_swap(int2* a, int2* b) { const int2 t = *a; *a = *b; *b = t; }
+
+VO_DEV void rb_move_median_to_first(int2* result, int2* a, int2* b, int2* c)
+{
+    if (rb_gt(*a, *b)) {
+        if (rb_gt(*b, *c)) rb_swap(result, b);
+        else if (rb_gt(*a, *c)) rb_swap(result, c);
+        else rb_swap(result, a);
+    } else if (rb_gt(*a, *c)) rb_swap(result, a);
+    else if (rb_gt(*b, *c)) rb_swap(result, c);
+    else rb_swap(result, b);
+}
+
+VO_DEV void rb_adjust_heap(int2* first, int hole, int len, int2 value)
+{
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (rb_gt(first[second], first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;                                   // __push_heap
+    while (hole > top && rb_gt(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+VO_DEV void rb_heap_select(int2* first, int2* middle, int2* last)
+{
+    const int len = (int)(middle - first);
+    if (len >= 2)
+        for (int parent = (len - 2) / 2;; --parent) {
+            rb_adjust_heap(first, parent, len, first[parent]);
+            if (parent == 0) break;
+        }
+    for (int2* i = middle; i < last; ++i)
+        if (rb_gt(*i, *first)) {
+            const int2 v = *i;
+            *i = *first;
+            rb_adjust_heap(first, 0, len, v);
+        }
+}
+
+VO_DEV void rb_insertion_sort(int2* first, int2* last)
+{
+    if (first == last) return;
+    for (int2* i = first + 1; i != last; ++i) {
+        const int2 v = *i;
+        if (rb_gt(v, *first)) {
+            for (int2* p = i; p != first; --p) *p = *(p - 1);
+            *first = v;
+        } else {
+            int2* hole = i;
+            int2* nx = i - 1;
+            while (rb_gt(v, *nx)) { *hole = *nx; hole = nx; --nx; }
+            *hole = v;
+        }
+    }
+}
+
+// Stopper lists of the pair-swap partition of rec[a, b): LP ascending positions with
+// lstop(r), RP descending positions with rstop(r); returns K = number of pairs
+// (LP[k], RP[k]) with LP[k] < RP[k], after swapping them.  rsent >= 0 appends that position
+// to RP (the unguarded scan's pivot sentinel).  Every thread returns the same values.
+template <class LS, class RS>
+VO_DEV int rb_pairs(int2* rec, int a, int b, LS lstop, RS rstop, int rsent, int* LP, int* RP, int* lds, int* nl_out,
+                    int* nr_out)
+{
+    const int tid = threadIdx.x;
+    int nL = 0, nR = 0;
+    for (int base = a; base < b; base += RB_T) {
+        const int p = base + tid;
+        const bool f = p < b && lstop(__int_as_float(rec[p].x));
+        int tot;
+        const int pos = block_scan_flag(f, lds, &tot);
+        if (f) LP[nL + pos] = p;
+        nL += tot;
+    }
+    for (int base = 0; base < b - a; base += RB_T) {
+        const int q = b - 1 - base - tid;
+        const bool f = q >= a && rstop(__int_as_float(rec[q].x));
+        int tot;
+        const int pos = block_scan_flag(f, lds, &tot);
+        if (f) RP[nR + pos] = q;
+        nR += tot;
+    }
+    if (rsent >= 0) {
+        if (tid == 0) RP[nR] = rsent;
+        ++nR;
+    }
+    __syncthreads();
+    // K: the pairs are ordered (LP ascending, RP descending), so LP[k] < RP[k] holds for a prefix
+    const int m = nL < nR ? nL : nR;
+    int cnt = 0;
+    for (int k = tid; k < m; k += RB_T) cnt += LP[k] < RP[k] ? 1 : 0;
+    int K;
+    block_scan_i32(cnt, lds, &K);
+    for (int k = tid; k < K; k += RB_T) rb_swap(&rec[LP[k]], &rec[RP[k]]);
+    __syncthreads();
+    *nl_out = nL;
+    *nr_out = nR;
+    return K;
+}
+
+__global__ void __launch_bounds__(RB_T) k_sift_retain_best(vo_sift_buf sb)
+{
+    const SiftImg im = sift_img(sb, blockIdx.z);
+    const int n = im.counters[2];
+    const int P = sb.nfeatures;
+    if (P <= 0 || n <= P) return;                                  // retainBest keeps everything
+    __shared__ int lds[16];
+    __shared__ int bc[2];
+    const int tid = threadIdx.x;
+    int2* rec = reinterpret_cast<int2*>(im.cand);
+    int* LP = im.cand + 2 * n;
+    int* RP = LP + n + 1;
+    for (int i = tid; i < n; i += RB_T) rec[i] = make_int2(__float_as_int(im.kp_out[6 * (int64_t)i + 4]), i);
+    __syncthreads();
+    // std::nth_element(first, first + P - 1, last): __introselect with depth 2 * __lg(n)
+    const int nth = P - 1;
+    int first = 0, last = n, depth = 2 * (31 - __clz(n));
+    bool heap = false;
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (tid == 0) {
+                rb_heap_select(rec + first, rec + nth + 1, rec + last);
+                rb_swap(rec + first, rec + nth);
+            }
+            heap = true;
+            break;
+        }
+        --depth;
+        if (tid == 0)                                              // __unguarded_partition_pivot
+            rb_move_median_to_first(rec + first, rec + first + 1, rec + first + (last - first) / 2, rec + last - 1);
+        __syncthreads();
+        const float pv = __int_as_float(rec[first].x);
+        int nL, nR;
+        const int K = rb_pairs(
+            rec, first + 1, last, [pv](float r) { return !(r > pv); }, [pv](float r) { return !(pv > r); }, first, LP,
+            RP, lds, &nL, &nR);
+        if (tid == 0) {
+            // i stops at L_{K+1}, or at R_K (it now holds a left stopper) if that comes first
+            int cut = K < nL ? LP[K] : last;
+            if (K > 0 && RP[K - 1] < cut) cut = RP[K - 1];
+            bc[0] = cut;
+        }
+        __syncthreads();
+        const int cut = bc[0];
+        __syncthreads();
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    if (!heap && tid == 0) rb_insertion_sort(rec + first, rec + last);
+    __syncthreads();
+    // std::partition(first + P, last, response >= kp[P - 1].response), then resize
+    const float amb = __int_as_float(rec[nth].x);
+    int nL, nR;
+    rb_pairs(
+        rec, P, n, [amb](float r) { return !(r >= amb); }, [amb](float r) { return r >= amb; }, -1, LP, RP, lds, &nL,
+        &nR);
+    const int kept = n - nL;                                       // every non-stopper is kept
+    // gather the kept rows in their new order (through the raw keypoint buffer, free now)
+    float* tmp = im.kp;
+    for (int i = tid; i < kept * 6; i += RB_T) tmp[i] = im.kp_out[6 * (int64_t)rec[i / 6].y + i % 6];
+    __syncthreads();
+    for (int i = tid; i < kept * 6; i += RB_T) im.kp_out[i] = tmp[i];
+    if (tid == 0) im.counters[2] = kept;
 }
 
 __global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
@@ -1398,6 +1601,7 @@ extern "C" int vo_sift_plan(vo_sift_buf* sb, int W, int H)
     if (!sb || W < 1 || H < 1) return VO_EARG;
     sb->W = W;
     sb->H = H;
+    sb->nfeatures = 0;
     const int bw = 2 * W, bh = 2 * H;
     const int mn = bw < bh ? bw : bh;
     int n_oct = (int)lrint(log((double)mn) / log(2.) - 2) + 1;
@@ -1440,7 +1644,8 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
                              vo_stream_t stream)
 {
     if (!sb || !imgs || B < 1 || B > 65535 || sb->W != W || sb->H != H || !sb->gauss || !sb->dog || !sb->tmp ||
-        !sb->consts || img_stride < (int64_t)W * H)
+        !sb->consts || img_stride < (int64_t)W * H || sb->kp_cap < 1 || sb->kp_cap > SORT_N || sb->nfeatures < 0 ||
+        (sb->nfeatures > 0 && (int64_t)sb->cand_cap * 4 < 4 * (int64_t)sb->kp_cap + 2))
         return VO_EARG;
     hipStream_t st = VO_STREAM(stream);
     // host-side constants with the C library's exp/pow (as the oracle): kernel 0 = base blur,
@@ -1541,6 +1746,8 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
         hipLaunchKernelGGL(k_sift_ori, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
     }
     hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1, 1, nb), dim3(1024), 0, st, *sb);
+    if (sb->nfeatures > 0)
+        hipLaunchKernelGGL(k_sift_retain_best, dim3(1, 1, nb), dim3(RB_T), 0, st, *sb);
     // wave-per-keypoint descriptor kernel unless VO_SIFT_DESC_SERIAL=1 (thread per keypoint;
     // both produce identical descriptors)
     const char* ser = getenv("VO_SIFT_DESC_SERIAL");

@@ -239,25 +239,30 @@ _SIFTS: dict = {}
 
 
 class _SIFT:
+    def __init__(self, nfeatures: int = 0):
+        self.nfeatures = int(nfeatures)
+
     def detectAndCompute(self, image, mask):
         from .features import Sift
         if mask is not None:
             raise NotImplementedError("mask is not used by the reference (:226 passes None)")
         img = _gray(image)
         H, W = img.shape
-        s = _SIFTS.get((W, H))
+        s = _SIFTS.get((W, H, self.nfeatures))
         if s is None:
-            s = _SIFTS[(W, H)] = Sift(W, H, _dev())
+            s = _SIFTS[(W, H, self.nfeatures)] = Sift(W, H, _dev(), nfeatures=self.nfeatures)
         s.run(torch.from_numpy(img).to(_dev()))
         kp, desc = s.result()
         kps = tuple(KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp)
         return kps, (desc.copy() if len(kps) else None)
 
 
-def SIFT_create(*args, **kwargs):
-    if args or kwargs:
-        raise NotImplementedError("the reference uses the default SIFT (:35)")
-    return _SIFT()
+def SIFT_create(nfeatures=0, *args, **kwargs):
+    """SIFT_create() (:35) or SIFT_create(nfeatures) (KeyPointsFilter::retainBest cap, BASELINE C5);
+    the other SIFT parameters keep OpenCV's defaults."""
+    if args or kwargs or int(nfeatures) < 0:
+        raise NotImplementedError("only nfeatures may be set (the reference uses the default SIFT, :35)")
+    return _SIFT(nfeatures)
 
 
 class _BFMatcher:

@@ -245,13 +245,6 @@ class Engine:
         launching thread right before (end=False) and after (end=True) each stage, with
         the torch stream that stage runs on (bench.py records HIP events there)."""
         frames = self._frames(frames)
-        la = getattr(self, "_la", None)
-        if la is not None:
-            # leaving lookahead mode: the pyramid built ahead may still be in flight into the
-            # buffer this step rebuilds; the state already points at (potential_frame, that buffer)
-            if la["ready"] is not None:
-                torch.cuda.current_stream(self.device).wait_event(la["ready"])
-            self._la = None
         self._step_launch(frames, self.prev, marks)
         self.prev = 1 - self.prev
 
@@ -259,66 +252,12 @@ class Engine:
         if os.environ.get("VO_ONE_STREAM") == "1":      # profiling: every stage on the main stream
             return torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device, priority=getattr(self, "side_priority", 0))
+            self._side = torch.cuda.Stream(self.device)
         return self._side
 
-    # ------------------------------------------------------------------ pyramid lookahead
-    def step_ahead(self, frames, frames_next, marks=None):
-        """step(frames) with one frame of pyramid lookahead (a streaming pipeline): this frame's
-        pyramid + Scharr derivatives were built during the previous step, and the pyramid of
-        ``frames_next`` is built during this one, on the GFTT side stream ahead of this frame's
-        GFTT.  Every step still builds exactly one pyramid; tracking then never waits for the
-        new frame's pyramid, which otherwise runs between two LK launches.  Three physical
-        pyramid buffers rotate through the roles previous / current / next; the state's
-        pyr[0] / pyr[1] are re-pointed before every step (prev = 0), so ``self.prev`` and the
-        state keep their usual meaning between steps, and step() may follow (it leaves
-        lookahead mode).  Results are identical to step().  Not for captured graphs
-        (capture_step binds the buffers it saw at capture time)."""
-        frames = self._frames(frames)
-        frames_next = self._frames(frames_next)
-        T = self.t
-        if getattr(self, "_la", None) is None:
-            for k in ("pyr", "der"):
-                if k + "2" not in T:
-                    T[k + "2"] = torch.zeros_like(T[k + "0"])
-            la = L.VoState()
-            for name in L._STATE_FIELDS:
-                setattr(la, name, getattr(self.state, name))
-            # physical buffers in the roles (prev, cur, next); prev holds potential_frame.  The
-            # state may point at any of the three (an earlier lookahead run rotated them)
-            phys = {T["pyr%d" % k].data_ptr(): k for k in range(3)}
-            p_prev = phys[getattr(self.state, "pyr%d" % self.prev)]
-            p_cur = phys[getattr(self.state, "pyr%d" % (1 - self.prev))]
-            roles = [p_prev, p_cur, 3 - p_prev - p_cur]
-            self._la = {"state": la, "ps": C.byref(la), "roles": roles, "ready": None, "frames": None}
-            # prologue: this frame's pyramid into the `cur` buffer, in stream order
-            self._la_point(la, 0, roles[1])
-            self._chk(self.lib.vo_pyr_build(self._pd, self._la["ps"], 0, C.c_void_p(frames.data_ptr()),
-                                            self.W * self.H, self.stream), "vo_pyr_build")
-        st = self._la
-        roles = st["roles"]
-        main = torch.cuda.current_stream(self.device)
-        if st["ready"] is not None:
-            main.wait_event(st["ready"])                 # this frame's pyramid (built last step)
-        self._la_point(self.state, 0, roles[0])
-        self._la_point(self.state, 1, roles[1])
-        self._la_point(st["state"], 0, roles[2])
-        st["frames"] = frames_next                       # alive until the side stream used it
-        self._step_launch(frames, 0, marks, ahead=frames_next)
-        st["roles"] = [roles[1], roles[2], roles[0]]
-        self.prev = 0
-        # between steps the state shows (potential_frame, next frame) as pyr[0], pyr[1]
-        self._la_point(self.state, 0, st["roles"][0])
-        self._la_point(self.state, 1, st["roles"][1])
-
-    def _la_point(self, state, slot, phys):
-        T = self.t
-        setattr(state, "pyr%d" % slot, T["pyr%d" % phys].data_ptr())
-        setattr(state, "der%d" % slot, T["der%d" % phys].data_ptr())
-
-    def _step_launch(self, frames, prev, marks=None, ahead=None):
+    def _step_launch(self, frames, prev, marks=None):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
-        new frame (pyr[cur], der[cur]) -> track(prev) -> PnP -> triangulate -> [join] ->
+        new frame (pyr[cur], der[cur]) -> track(prev) -> PnP + triangulate -> [join] ->
         add_finish.  side: GFTT on the new frame (needs only its pyramid,
         VisualOdometryPipeLine.py:253), overlapping tracking and PnP.  GFTT never writes the
         chain status (PnP owns it while the two run; see k_gftt_select)."""
@@ -339,40 +278,11 @@ class Engine:
                 marks(i, True, strm)
 
         forked = side.cuda_stream != main.cuda_stream
-        if ahead is None:
-            run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
-            if forked:
-                side.wait_stream(main)                            # pyramid(cur) ready
-        else:
-            # lookahead: pyr(cur) is ready (step_ahead waited for it); the next frame's pyramid
-            # goes into the buffer the previous step's tracking released, on the side stream
-            # ahead of this frame's GFTT
-            if forked:
-                side.wait_stream(main)
-            la = self._la
-            fn = C.c_void_p(ahead.data_ptr())
-            # VO_LA_STREAM=own: on a stream of its own (GFTT does not wait for it)
-            if forked and os.environ.get("VO_LA_STREAM") == "own":
-                if la.get("stream") is None:
-                    la["stream"] = torch.cuda.Stream(self.device)
-                ls = la["stream"]
-                ls.wait_stream(main)
-            else:
-                ls = side
-            run(0, ls, lambda: lib.vo_pyr_build(pd, la["ps"], 0, fn, self.W * self.H, C.c_void_p(ls.cuda_stream)))
-            ev = torch.cuda.Event()
-            ev.record(ls)
-            la["ready"] = ev
+        run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
+        if forked:
+            side.wait_stream(main)                                # pyramid(cur) ready
         run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
-        bulk = getattr(self, "bulk_stream", None)
-        if bulk is not None:
-            # LK on a CU-masked stream (set by the caller, see cu_masked_stream)
-            sb = C.c_void_p(bulk.cuda_stream)
-            bulk.wait_stream(main)
-            run(1, bulk, lambda: lib.vo_track(pd, po, ps, prev, sb))
-            main.wait_stream(bulk)
-        else:
-            run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
+        run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
         if getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1"):
             # one launch for both stages (vo_pnp_triangulate); stage 3 is then empty
             run(2, main, lambda: lib.vo_pnp_triangulate(pd, po, ps, sm))
@@ -423,13 +333,14 @@ class Engine:
         """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:
         SIFT on both frames, BF 2-NN + ratio test, 5-point E-RANSAC, inlier split,
         recoverPose, t *= sign(t_z), triangulation, pose append; then potential_frame
-        = img1 (its pyramid + derivatives become pyr[prev]).
+        = img1 (its pyramid + derivatives become pyr[prev]).  Option ``sift_nfeatures`` (the C5
+        preset's 8192) is SIFT_create(nfeatures).
 
         Batched across chains: the chains are taken in chunks whose SIFT scale spaces fit
         ``sift_batch_bytes`` (default 12 GB, env VO_SIFT_BATCH_BYTES); per chunk one
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync until
-        the capacity check at the end."""
+        the SIFT capacity check, which comes before any chain state is written."""
         from .features import Sift, bf_knn2_batch
         img0 = self._frames(img0)
         img1 = self._frames(img1)
@@ -439,10 +350,11 @@ class Engine:
         budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 12 << 30))
         per_img = Sift.bytes_per_image(self.W, self.H)
         m = max(1, min(B, budget // (2 * per_img)))          # chains per chunk
-        if getattr(self, "_sift", None) is None or self._sift.batch < 2 * m:
+        nfeat = int(self.options.get("sift_nfeatures", 0))    # C5: SIFT_create(8192)
+        if getattr(self, "_sift", None) is None or self._sift.batch < 2 * m or self._sift.nfeatures != nfeat:
             self._sift = None
             torch.cuda.empty_cache()
-            self._sift = Sift(self.W, self.H, dev, batch=2 * m)
+            self._sift = Sift(self.W, self.H, dev, batch=2 * m, nfeatures=nfeat)
         sift = self._sift
         kcap = sift.kp_cap
         cap = min(d.ncap, d.pcap, kcap)
@@ -466,13 +378,15 @@ class Engine:
                                                 C.c_void_p(n[:k].data_ptr()), kcap, float(self.opts.feature_ratio),
                                                 C.c_void_p(pts0[c0:c1].data_ptr()), C.c_void_p(pts1[c0:c1].data_ptr()),
                                                 C.c_void_p(cnt[c0:c1].data_ptr()), cap, st), "vo_ratio_matches")
+        # one host sync before any chain state is touched: a truncated keypoint or match set
+        # must not bootstrap a chain
+        if int(overflow):
+            raise RuntimeError("SIFT capacity exceeded")
         self._chk(self.lib.vo_bootstrap(self._pd, self._po, self._ps, C.c_void_p(pts0.data_ptr()),
                                         C.c_void_p(pts1.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, st),
                   "vo_bootstrap")
         self.prev = 0
         self.build_pyramid(img1, self.prev)
-        if int(overflow):
-            raise RuntimeError("SIFT capacity exceeded")
         self._boot_debug = {"n0": n0, "n1": n1, "pts0": pts0, "pts1": pts1, "cnt": cnt}
 
     # ------------------------------------------------------------------ state I/O
@@ -552,36 +466,3 @@ class Engine:
         planes = [t[q * d.pyr_stride + o:q * d.pyr_stride + o + n].view(h + 2 * L.VO_BORDER, p) for q in (0, 1)]
         buf = torch.stack(planes, dim=-1)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()
-
-
-def reserve_mask(n_cus: int, reserve: int) -> list:
-    """CU-mask words with `reserve` CUs cleared, spread evenly over the XCDs whether the
-    driver numbers CUs XCD-contiguously (CU i on XCD i // (n/8)) or round-robin (XCD i % 8):
-    the cleared CUs are 33*j + 8*m (j = 0..7, m = 0..reserve/8-1) for 256 CUs."""
-    bits = [1] * n_cus
-    per = max(1, reserve // 8)
-    for j in range(8):
-        for m in range(per):
-            i = (n_cus // 8 + 1) * j + 8 * m
-            if i < n_cus:
-                bits[i] = 0
-    words = [0] * ((n_cus + 31) // 32)
-    for i, b in enumerate(bits):
-        if b:
-            words[i // 32] |= 1 << (i % 32)
-    return words
-
-
-def cu_masked_stream(device, reserve: int):
-    """A torch stream (wrapping a HIP stream from vo_stream_create_cumask) that launches on
-    every CU but `reserve` of them; returns (stream, handle) -- release with
-    lib().vo_stream_destroy(handle) after the last use."""
-    lib = L.lib()
-    n = lib.vo_device_cus()
-    if n <= 0:
-        raise RuntimeError("vo_device_cus failed")
-    words = reserve_mask(n, reserve)
-    arr = (C.c_uint32 * len(words))(*words)
-    h = C.c_void_p()
-    L.check(lib.vo_stream_create_cumask(len(words), arr, C.byref(h)), "vo_stream_create_cumask")
-    return torch.cuda.ExternalStream(h.value, device=device), h

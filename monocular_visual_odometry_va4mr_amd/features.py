@@ -11,13 +11,22 @@ import torch
 from . import _lib as L
 
 
-class Sift:
-    """SIFT for one image size on one device (OpenCV 4.6 defaults), ``batch`` images per
-    launch sequence (vo_sift_batch).  Buffers hold ``batch`` per-image blocks: results of
-    image b are kp_out[b], desc[b], counters[b, 2]."""
+def default_kp_cap(width: int, height: int) -> int:
+    """Raw keypoints held per image (sorted in LDS: at most 32,768): 16,384 up to a megapixel,
+    32,768 above (the dense C5 1920x1080 scene yields ~16k keypoints after deduplication)."""
+    return 16384 if int(width) * int(height) <= (1 << 20) else 32768
 
-    def __init__(self, width: int, height: int, device=None, cand_cap: int = 131072, kp_cap: int = 16384,
-                 batch: int = 1):
+
+class Sift:
+    """SIFT for one image size on one device (OpenCV 4.6 defaults; ``nfeatures`` > 0 is
+    SIFT_create(nfeatures), BASELINE C5's capped SIFT), ``batch`` images per launch sequence
+    (vo_sift_batch).  Buffers hold ``batch`` per-image blocks: results of image b are
+    kp_out[b], desc[b], counters[b, 2]."""
+
+    def __init__(self, width: int, height: int, device=None, cand_cap: int = 131072, kp_cap: int | None = None,
+                 batch: int = 1, nfeatures: int = 0):
+        if kp_cap is None:
+            kp_cap = default_kp_cap(width, height)
         self.lib = L.lib()
         self.device = torch.device(device or "cuda")
         self.W, self.H = int(width), int(height)
@@ -41,11 +50,15 @@ class Sift:
         for k, v in self.t.items():
             setattr(sb, k, v.data_ptr())
         sb.cand_cap, sb.kp_cap = int(cand_cap), int(kp_cap)
+        sb.nfeatures = int(nfeatures)
+        self.nfeatures = int(nfeatures)
         self.sb = sb
         self.kp_cap = int(kp_cap)
 
     @staticmethod
-    def bytes_per_image(width: int, height: int, cand_cap: int = 131072, kp_cap: int = 16384) -> int:
+    def bytes_per_image(width: int, height: int, cand_cap: int = 131072, kp_cap: int | None = None) -> int:
+        if kp_cap is None:
+            kp_cap = default_kp_cap(width, height)
         sb = L.VoSiftBuf()
         L.check(L.lib().vo_sift_plan(C.byref(sb), int(width), int(height)), "vo_sift_plan")
         return 4 * (sb.gauss_floats + sb.dog_floats + sb.tmp_floats + 8 + cand_cap * 4 + kp_cap * (8 + 6 + 128 + 360))

@@ -89,16 +89,17 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     t_boot = time.perf_counter() - t0
     # status of every chain at its shard's own last step (chains whose shard has ended keep
     # re-reading their last frame until the longest shard is done; what happens to them then
-    # does not count).  Kept on the device: no host sync inside the loop.
+    # does not count; a shard with no step keeps its bootstrap status, the clone below).
+    # Kept on the device: no host sync inside the loop.
     last_step = torch.tensor([s.n_steps - 1 for s in mine], device=dev)
     final_status = eng.t["status"].clone()
     for j in range(n_steps):
         eng.step(frames_at([min(s.boot1 + 1 + j, s.end - 1) for s in mine]))
         final_status = torch.where(last_step == j, eng.t["status"], final_status)
-    final_status = torch.where(last_step < 0, eng.t["status"], final_status)
     _sync(dev)
     wall = time.perf_counter() - t0
     t_step = wall - t_boot
+    t_g = time.perf_counter()
     packed = Sh.pack_poses(eng.t["pose_R"], eng.t["pose_t"], eng.t["nF"], eng.dims.fcap)
     allp = Sh.gather_poses(packed)
     import torch.distributed as dist
@@ -106,13 +107,16 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
         st_all = [torch.empty_like(final_status) for _ in range(world)]
         dist.all_gather(st_all, final_status.contiguous())
         statuses = torch.cat(st_all).cpu().numpy()
-        tt = torch.tensor([t_step, wall, t_boot], dtype=torch.float64, device=dev)
+        t_gather = time.perf_counter() - t_g
+        tt = torch.tensor([t_step, wall, t_boot, t_gather], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step, wall, t_boot = (float(v) for v in tt.cpu())
+        t_step, wall, t_boot, t_gather = (float(v) for v in tt.cpu())
     else:
         statuses = final_status.cpu().numpy()
+        t_gather = time.perf_counter() - t_g
     if allp is None:
         return None
+    t_s = time.perf_counter()
     allp = allp.cpu().numpy()
     centres = [Sh.unpack_centres(chain)[: s.end - s.boot1 + 1] for s, chain in zip(plan, allp)]
     ok_shards, ok_centres, failed = [], [], []
@@ -123,6 +127,7 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
         else:
             failed.append({"shard": s.index, "status": int(st), "poses": int(len(c))})
     stitched = Sh.stitch(ok_shards, ok_centres) if ok_shards else None
+    t_stitch = time.perf_counter() - t_s
     rep = Ev.shard_report(ok_shards, ok_centres, cs, stitched, reference=reference)
     frames_done = sum(s.n_steps for s in plan)
     per = rep["shards"]
@@ -133,6 +138,9 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
         "sequence_frames_per_s": round(n_frames / max(wall, 1e-9), 1),
         "step_frames_per_s": round(frames_done / max(t_step, 1e-9), 1),
         "wall_s": round(wall, 3), "bootstrap_s": round(t_boot, 3), "step_s": round(t_step, 3),
+        # after the clock: pose gather (the collective) and the Sim(3) stitch on rank 0
+        "gather_ms": round(t_gather * 1e3, 3), "stitch_ms": round(t_stitch * 1e3, 3),
+        "job_frames_per_s": round(n_frames / max(wall + t_gather + t_stitch, 1e-9), 1),
         "shard_ate_rel_max": max((p["ate_rel"] for p in per), default=None),
         "stitched": rep.get("stitched"),
     }

@@ -15,7 +15,7 @@ footprint so that far surfaces fade to the mean instead of aliasing.  The camera
 moves forward one unit per frame and yaws sinusoidally (bounded lateral drift).
 
 The KITTI-size (C2) sequence uses its own scene (``PRESET_SCENES``): half a unit per
-frame, seven texture octaves and no distance fading.  With the default scene the
+frame, seven texture octaves and no distance fading; the 1920x1080 (C5) sequence uses it too.  With the default scene the
 reference orchestration loses every landmark after a few hundred frames (its monocular
 scale collapses until the 1-unit minimum-depth gate rejects every triangulation,
 VisualOdometryPipeLine.py:149-168); with this one it tracks all 4541 frames from frame 0
@@ -97,6 +97,10 @@ class SceneParams:
 # scene per sequence preset (default SceneParams() otherwise); see the module docstring
 PRESET_SCENES = {
     "kitti": SceneParams(speed=0.5, octaves=7, lod=False),
+    # C5 (BASELINE "8k keypoints/frame"): the C2 scene at 1920x1080 -- ~16k SIFT keypoints per
+    # frame, so the bootstrap's SIFT_create(nfeatures=8192) cap is exercised, and a full 8,192
+    # GFTT corners (the default scene gave 4.4k SIFT keypoints and ~6.5k corners)
+    "hd1080": SceneParams(speed=0.5, octaves=7, lod=False),
 }
 
 

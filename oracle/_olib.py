@@ -50,6 +50,9 @@ def _declare(L):
     L.vo_o_five_point.argtypes = [P, P, P]
     L.vo_o_recover_pose.argtypes = [P, P, P, I, P, P, P, P, P]
     L.vo_o_sift.argtypes = [P, I, I, P, P, I, P]
+    L.vo_o_sift_n.argtypes = [P, I, I, I, P, P, I, P]
+    L.vo_o_retain_best.argtypes = [P, I, I, P]
+    L.vo_o_retain_best_heap_selects.argtypes = []
     L.vo_o_bf_knn2.argtypes = [P, I, P, I, I, P, P]
     L.vo_o_set_fp32_mode.argtypes = [I]
     L.vo_o_set_fp32_mode.restype = None
@@ -233,16 +236,29 @@ def recover_pose(E, p0, p1, K):
     return ng.value, R, t, mask[:n].copy()
 
 
-def sift(img, cap=200000):
+def sift(img, cap=None, nfeatures=0):
+    """SIFT_create(nfeatures).detectAndCompute(img, None): (kp [n,6], desc [n,128])."""
     img = c_u8(img)
     h, w = img.shape
     n = C.c_int(0)
-    lib().vo_o_sift(ptr(img), w, h, None, None, 0, C.byref(n))
-    cap = n.value
-    kp = np.zeros((max(cap, 1), 6), np.float32)
-    desc = np.zeros((max(cap, 1), 128), np.float32)
-    lib().vo_o_sift(ptr(img), w, h, ptr(kp), ptr(desc), cap, C.byref(n))
-    return kp[:cap].copy(), desc[:cap].copy()
+    cap = 32768 if cap is None else int(cap)
+    while True:
+        kp = np.zeros((max(cap, 1), 6), np.float32)
+        desc = np.zeros((max(cap, 1), 128), np.float32)
+        lib().vo_o_sift_n(ptr(img), w, h, int(nfeatures), ptr(kp), ptr(desc), cap, C.byref(n))
+        if n.value <= cap:
+            return kp[:n.value].copy(), desc[:n.value].copy()
+        cap = n.value
+
+
+def retain_best(response, n_points):
+    """KeyPointsFilter::retainBest on a response array: (perm [n] i32, kept)."""
+    r = c_f32(response).reshape(-1)
+    perm = np.zeros((max(len(r), 1),), np.int32)
+    kept = lib().vo_o_retain_best(ptr(r), len(r), int(n_points), ptr(perm))
+    if kept < 0:
+        raise RuntimeError("vo_o_retain_best failed")
+    return perm[:len(r)].copy(), int(kept)
 
 
 def bf_knn2(q, t):

@@ -57,21 +57,24 @@ class DMatch:
 
 
 class _SIFT:
+    def __init__(self, nfeatures=0):
+        self.nfeatures = int(nfeatures)
+
     def detectAndCompute(self, image, mask):
         if mask is not None:
             raise NotImplementedError("mask not supported (the reference passes None)")
         img = np.asarray(image)
         if img.ndim != 2 or img.dtype != np.uint8:
             raise error("SIFT oracle expects a uint8 grayscale image")
-        kp, desc = O.sift(img)
+        kp, desc = O.sift(img, nfeatures=self.nfeatures)
         kps = tuple(KeyPoint(k[0], k[1], k[2], k[3], k[4], int(k[5])) for k in kp)
         return kps, (desc if len(kps) else None)
 
 
-def SIFT_create(*args, **kwargs):
-    if args or kwargs:
-        raise NotImplementedError("only the default SIFT is used by the reference (:35)")
-    return _SIFT()
+def SIFT_create(nfeatures=0, *args, **kwargs):
+    if args or kwargs or int(nfeatures) < 0:
+        raise NotImplementedError("only nfeatures may be set (the reference uses the default SIFT, :35)")
+    return _SIFT(nfeatures)
 
 
 class _BFMatcher:

@@ -16,6 +16,7 @@
 
 #include <float.h>
 #include <limits.h>
+#include <stddef.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -434,7 +435,188 @@ static int kp_cmp(const void* pa, const void* pb)
     return 0;
 }
 
+/* ------------------------------------------------ KeyPointsFilter::retainBest
+ * OpenCV 4.6 features2d/src/keypoint.cpp:
+ *     std::nth_element(kp.begin(), kp.begin() + n_points - 1, kp.end(), KeypointResponseGreater());
+ *     float ambiguous_response = kp[n_points - 1].response;
+ *     new_end = std::partition(kp.begin() + n_points, kp.end(),
+ *                              KeypointResponseGreaterThanOrEqualToThreshold(ambiguous_response));
+ *     kp.resize(new_end - kp.begin());
+ * The order the kept keypoints end up in (the BF query order downstream) is whatever
+ * libstdc++'s algorithms leave; opencv-python wheels are built with GCC, so this restates
+ * bits/stl_algo.h (__introselect, __unguarded_partition_pivot, __move_median_to_first,
+ * __unguarded_partition, __heap_select, __insertion_sort, __unguarded_linear_insert, the
+ * bidirectional __partition) and bits/stl_heap.h (__make_heap, __adjust_heap, __push_heap,
+ * __pop_heap) step for step.  tests/test_retain_best.py checks it against std::nth_element
+ * and std::partition compiled by this image's g++.  Elements carry (response, index);
+ * comparisons read the response only, as KeypointResponseGreater does. */
+typedef struct { float r; int32_t i; } rb_t;
+#define RB_GT(a, b) ((a).r > (b).r)     /* KeypointResponseGreater */
+
+static void rb_swap(rb_t* a, rb_t* b) { rb_t t = *a; *a = *b; *b = t; }
+
+static void rb_move_median_to_first(rb_t* result, rb_t* a, rb_t* b, rb_t* c)
+{
+    if (RB_GT(*a, *b)) {
+        if (RB_GT(*b, *c)) rb_swap(result, b);
+        else if (RB_GT(*a, *c)) rb_swap(result, c);
+        else rb_swap(result, a);
+    } else if (RB_GT(*a, *c)) rb_swap(result, a);
+    else if (RB_GT(*b, *c)) rb_swap(result, c);
+    else rb_swap(result, b);
+}
+
+static rb_t* rb_unguarded_partition(rb_t* first, rb_t* last, const rb_t* pivot)
+{
+    for (;;) {
+        while (RB_GT(*first, *pivot)) ++first;
+        --last;
+        while (RB_GT(*pivot, *last)) --last;
+        if (!(first < last)) return first;
+        rb_swap(first, last);
+        ++first;
+    }
+}
+
+static rb_t* rb_unguarded_partition_pivot(rb_t* first, rb_t* last)
+{
+    rb_t* mid = first + (last - first) / 2;
+    rb_move_median_to_first(first, first + 1, mid, last - 1);
+    return rb_unguarded_partition(first + 1, last, first);
+}
+
+static void rb_push_heap(rb_t* first, ptrdiff_t hole, ptrdiff_t top, rb_t value)
+{
+    ptrdiff_t parent = (hole - 1) / 2;
+    while (hole > top && RB_GT(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+static void rb_adjust_heap(rb_t* first, ptrdiff_t hole, ptrdiff_t len, rb_t value)
+{
+    const ptrdiff_t top = hole;
+    ptrdiff_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (RB_GT(first[second], first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    rb_push_heap(first, hole, top, value);
+}
+
+static void rb_heap_select(rb_t* first, rb_t* middle, rb_t* last)
+{
+    const ptrdiff_t len = middle - first;
+    if (len >= 2) {                                            /* __make_heap */
+        for (ptrdiff_t parent = (len - 2) / 2;; --parent) {
+            rb_adjust_heap(first, parent, len, first[parent]);
+            if (parent == 0) break;
+        }
+    }
+    for (rb_t* i = middle; i < last; ++i)
+        if (RB_GT(*i, *first)) {                               /* __pop_heap(first, middle, i) */
+            rb_t v = *i;
+            *i = *first;
+            rb_adjust_heap(first, 0, len, v);
+        }
+}
+
+static void rb_insertion_sort(rb_t* first, rb_t* last)
+{
+    if (first == last) return;
+    for (rb_t* i = first + 1; i != last; ++i) {
+        rb_t v = *i;
+        if (RB_GT(v, *first)) {
+            memmove(first + 1, first, (size_t)(i - first) * sizeof(rb_t));
+            *first = v;
+        } else {                                               /* __unguarded_linear_insert */
+            rb_t* hole = i;
+            rb_t* nx = i - 1;
+            while (RB_GT(v, *nx)) { *hole = *nx; hole = nx; --nx; }
+            *hole = v;
+        }
+    }
+}
+
+static int g_rb_heap_selects = 0;     /* depth-limit fallbacks taken (tests) */
+int vo_o_retain_best_heap_selects(void) { return g_rb_heap_selects; }
+
+static void rb_introselect(rb_t* first, rb_t* nth, rb_t* last, int depth)
+{
+    while (last - first > 3) {
+        if (depth == 0) {
+            ++g_rb_heap_selects;
+            rb_heap_select(first, nth + 1, last);
+            rb_swap(first, nth);
+            return;
+        }
+        --depth;
+        rb_t* cut = rb_unguarded_partition_pivot(first, last);
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    rb_insertion_sort(first, last);
+}
+
+/* std::partition (bidirectional form), pred(x) = x.response >= thr */
+static rb_t* rb_partition_ge(rb_t* first, rb_t* last, float thr)
+{
+    for (;;) {
+        for (;;) {
+            if (first == last) return first;
+            if (first->r >= thr) ++first;
+            else break;
+        }
+        --last;
+        for (;;) {
+            if (first == last) return first;
+            if (!(last->r >= thr)) --last;
+            else break;
+        }
+        rb_swap(first, last);
+        ++first;
+    }
+}
+
+static size_t rb_retain_best(rb_t* kp, size_t n, int n_points)
+{
+    if (n_points < 0 || n <= (size_t)n_points) return n;
+    if (n_points == 0) return 0;
+    int lg = 0;                                                /* std::__lg */
+    for (size_t m = n; m > 1; m >>= 1) ++lg;
+    rb_introselect(kp, kp + n_points - 1, kp + n, 2 * lg);
+    const float amb = kp[n_points - 1].r;
+    return (size_t)(rb_partition_ge(kp + n_points, kp + n, amb) - kp);
+}
+
+int vo_o_retain_best(const float* response, int n, int n_points, int32_t* perm)
+{
+    if (n < 0 || (n > 0 && (!response || !perm))) return VO_O_EARG;
+    rb_t* a = (rb_t*)malloc(sizeof(rb_t) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; ++i) { a[i].r = response[i]; a[i].i = i; }
+    const size_t kept = rb_retain_best(a, (size_t)n, n_points);
+    for (int i = 0; i < n; ++i) perm[i] = a[i].i;
+    free(a);
+    return (int)kept;
+}
+
 int vo_o_sift(const uint8_t* image, int w, int h, float* kp_out, float* desc, int cap, int* n_out)
+{
+    return vo_o_sift_n(image, w, h, 0, kp_out, desc, cap, n_out);
+}
+
+int vo_o_sift_n(const uint8_t* image, int w, int h, int nfeatures, float* kp_out, float* desc, int cap,
+                int* n_out)
 {
     if (!image || w < 1 || h < 1 || !n_out) return VO_O_EARG;
     exptab_init();
@@ -536,6 +718,19 @@ int vo_o_sift(const uint8_t* image, int w, int h, float* kp_out, float* desc, in
                 kps[++a] = kps[b];
         }
         nk = a + 1;
+    }
+    /* SIFT_Impl::detectAndCompute: if (nfeatures > 0) KeyPointsFilter::retainBest(keypoints,
+     * nfeatures), between removeDuplicatedSorted and the firstOctave adjustment */
+    if (nfeatures > 0 && nk > (size_t)nfeatures) {
+        rb_t* a = (rb_t*)malloc(sizeof(rb_t) * nk);
+        for (size_t q = 0; q < nk; ++q) { a[q].r = kps[q].response; a[q].i = (int32_t)q; }
+        const size_t kept = rb_retain_best(a, nk, nfeatures);
+        kp_t* sel = (kp_t*)malloc(sizeof(kp_t) * (kept ? kept : 1));
+        for (size_t q = 0; q < kept; ++q) sel[q] = kps[a[q].i];
+        memcpy(kps, sel, sizeof(kp_t) * kept);
+        nk = kept;
+        free(sel);
+        free(a);
     }
     /* firstOctave = -1 adjustment */
     for (size_t q = 0; q < nk; ++q) {

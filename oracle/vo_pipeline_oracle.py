@@ -118,8 +118,9 @@ def triangulate_candidates(s: OracleState, R_cur_CW, t_cur_CW):
 
 
 def bootstrap_matches(s: OracleState, img0, img1):
-    """initial_feature_matching :209-245."""
-    sift = cv.SIFT_create()
+    """initial_feature_matching :209-245 (``sift_nfeatures``: the C5 benchmark's capped SIFT;
+    absent from the reference's option dicts, where SIFT_create() keeps every keypoint)."""
+    sift = cv.SIFT_create(int(s.opts.get('sift_nfeatures', 0)))
     k0, d0 = sift.detectAndCompute(img0, None)
     k1, d1 = sift.detectAndCompute(img1, None)
     pairs = cv.BFMatcher().knnMatch(d0, d1, k=2)

@@ -136,10 +136,10 @@ def test_essential_and_recover_pose():
     ok, Eo, mo = O.find_essential(a32, b32, K, 0.99, 1.0, 1000)
     assert ok and Eg is not None
     assert np.array_equal(mg.ravel(), mo)
-    assert np.abs(Eg - Eo).max() < 1e-9
+    assert np.array_equal(Eg, Eo)
     ng, Rg, tg, _ = G.recoverPose(Eg, a32, b32, K)
     no, Ro, to, _ = O.recover_pose(Eo, a32, b32, K)
-    assert ng == no and np.abs(Rg - Ro).max() < 1e-9 and np.abs(tg - to).max() < 1e-9
+    assert ng == no and np.array_equal(Rg, Ro) and np.array_equal(tg, to)
 
 
 def _oracle_init(case):

@@ -24,7 +24,7 @@ def test_parking_folder_run_matches_golden(tmp_path):
     vo = res["_vo"]
     t = np.array([np.asarray(x).ravel() for _, x in vo.transforms[1:]])
     assert res["frames"] == len(fr) - 7
-    assert np.abs(t - g["t"][:len(t), :, 0]).max() < 1e-6
+    assert np.array_equal(t, g["t"][:len(t), :, 0])
     assert np.array_equal(np.asarray(vo.num_pts), g["num_pts"][:len(vo.num_pts)])
     w, h, _, _ = ingest.png_info(open(png, "rb").read())
     assert (w, h) == (1000, 800)

@@ -33,4 +33,4 @@ def test_png_ingest_feeds_engine(tmp_path):
     for i in range(boot[1] + 1, len(fr)):
         eng.step(dev_frames[i])
     t = np.array([np.asarray(x).ravel() for _, x in eng.export_chain(0)["transforms"][1:]])
-    assert np.abs(t - g["t"][:len(t), :, 0]).max() < 1e-6
+    assert np.array_equal(t, g["t"][:len(t), :, 0])

@@ -129,6 +129,31 @@ def test_gftt_bitexact(kitti_frames, engine_factory):
         assert np.array_equal(e, O.eigmap(fr[1]))
 
 
+@pytest.mark.parametrize("harris,bs", [(True, 3), (False, 5), (False, 7), (True, 5), (True, 7)])
+def test_gftt_harris_blocksize_bitexact(kitti_frames, engine_factory, harris, bs):
+    """goodFeaturesToTrack with the reference's own option keys feature_use_harris /
+    feature_block_size (main.py:32-33 -> VisualOdometryPipeLine.py:256) away from the presets'
+    (False, 3): the Harris response det - k tr^2 and the generic blockSize box sums, C2 size,
+    corner list and eigen / Harris map bit for bit."""
+    from oracle import _olib as O
+    fr, K = kitti_frames
+    q = 0.01 if harris else 0.1        # Harris responses are far more peaked than min-eig
+    eng, opts = engine_factory(K=K, feature_use_harris=harris, feature_block_size=bs, feature_quality_level=q)
+    eng.build_pyramid(fr[1], 0)
+    L = eng.lib
+    assert L.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+    torch.cuda.synchronize()
+    n = int(eng.t["nCorners"][0])
+    got = eng.t["corners"][0, :n].cpu().numpy()
+    ref = O.gftt(fr[1], 1400, q, 10, bs, use_harris=harris)
+    assert len(ref) > 300
+    assert np.array_equal(got, ref), f"harris={harris} blockSize={bs}: {n} vs {len(ref)}"
+    assert L.vo_gftt_eigmap(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+    torch.cuda.synchronize()
+    e = eng.t["eig"][0].cpu().numpy().reshape(376, 1241)
+    assert np.array_equal(e, O.eigmap(fr[1], bs, use_harris=harris))
+
+
 def test_lk_bitexact(kitti_frames, engine_factory):
     from oracle import _olib as O
     fr, K = kitti_frames
