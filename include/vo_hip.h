@@ -46,8 +46,8 @@ enum vo_chain_status {
 #define VO_BORDER 16
 
 /* Geometry of the per-chain image pyramid: u8 images with a VO_BORDER reflect-101 border;
- * derivative images as two int16 planes (dx at [0, pyr_stride), dy at [pyr_stride,
- * 2*pyr_stride)) with a zero border, each at the pyramid's offsets and pitch in elements.
+ * derivative images as interleaved int16 (dx, dy) pairs with a zero border: the pixel at
+ * pyramid byte offset o has dx at der[2o] and dy at der[2o + 1] (one dword per pixel).
  * The engine gives every level the pitch of level 0 (the LK kernel relies on it for
  * scalar row offsets; other pitches select the per-level LK kernels). */
 typedef struct vo_dims {
@@ -56,7 +56,7 @@ typedef struct vo_dims {
     int32_t lvl_w[VO_MAX_LEVELS], lvl_h[VO_MAX_LEVELS], lvl_pitch[VO_MAX_LEVELS];
     int64_t lvl_off[VO_MAX_LEVELS];  /* byte offset of level l (padded origin)         */
     int64_t pyr_stride;           /* bytes per chain, u8 pyramid                          */
-    int64_t der_stride;           /* int16 elements per chain (>= 2*pyr_stride): dx, dy  */
+    int64_t der_stride;           /* int16 elements per chain (>= 2*pyr_stride): (dx, dy) */
     int32_t ncap, pcap, fcap;     /* landmark, candidate, pose capacities per chain       */
     int32_t ccap;                 /* GFTT local-maximum candidates per chain              */
     int32_t mcap;                 /* GFTT output corners per chain                        */

@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
 {
     __shared__ int cstart[ADD_MAX_CELLS + 1];
     __shared__ int cfill[ADD_MAX_CELLS];
-    __shared__ int items[ADD_MAX_ITEMS];
+    __shared__ int items_lds[ADD_MAX_ITEMS];
     __shared__ int lds[16];
     __shared__ int sh_scan[ADD_THREADS / 64];
     const int b = blockIdx.x, tid = threadIdx.x;
@@ -909,7 +909,12 @@ __global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
     int cs = (int)ceil(A.min_dist) > 0 ? (int)ceil(A.min_dist) : 1;
     while ((d.W / cs + 3) * (d.H / cs + 3) > ADD_MAX_CELLS) ++cs;
     const int gw = d.W / cs + 3, gh = d.H / cs + 3;
-    const bool grid = (gw * gh <= ADD_MAX_CELLS) && (P <= ADD_MAX_ITEMS);
+    // the cell-sorted candidate list lives in LDS, or for more than ADD_MAX_ITEMS candidates
+    // (C5: ~15k points per chain) in the chain's int scratch, free once PnP is done (same
+    // stream) -- the all-pairs fallback below is O(M * P)
+    int* items = items_lds;
+    if (P > ADD_MAX_ITEMS) items = s.iwork + (int64_t)b * d.iwork_stride;
+    const bool grid = (gw * gh <= ADD_MAX_CELLS) && (P <= ADD_MAX_ITEMS || P <= d.iwork_stride);
     if (grid) {
         for (int q = tid; q < gw * gh; q += blockDim.x) cfill[q] = 0;
         __syncthreads();

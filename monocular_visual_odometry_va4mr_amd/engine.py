@@ -148,7 +148,7 @@ class Engine:
         T = {}
         T["pyr0"] = z(B, d.pyr_stride, dt=torch.uint8)
         T["pyr1"] = z(B, d.pyr_stride, dt=torch.uint8)
-        T["der0"] = z(B, d.der_stride, dt=torch.int16)     # zero border is relied upon
+        T["der0"] = z(B, d.der_stride, dt=torch.int16)     # (dx, dy) pairs; zero border is relied upon
         T["der1"] = z(B, d.der_stride, dt=torch.int16)
         T["lm_X"] = z(B, ncap, 3, dt=torch.float32)
         T["lm_kp"] = z(B, ncap, 2, dt=torch.float32)
@@ -462,7 +462,6 @@ class Engine:
         which = self.prev if which is None else which
         w, h, p, o = d.lvl_w[level], d.lvl_h[level], d.lvl_pitch[level], d.lvl_off[level]
         n = (h + 2 * L.VO_BORDER) * p
-        t = self.t["der%d" % which][b]
-        planes = [t[q * d.pyr_stride + o:q * d.pyr_stride + o + n].view(h + 2 * L.VO_BORDER, p) for q in (0, 1)]
-        buf = torch.stack(planes, dim=-1)
+        # interleaved (dx, dy) int16 pairs: the pixel at pyramid byte offset o is der[2o], der[2o + 1]
+        buf = self.t["der%d" % which][b].view(-1, 2)[o:o + n].view(h + 2 * L.VO_BORDER, p, 2)
         return buf[L.VO_BORDER:L.VO_BORDER + h, L.VO_BORDER:L.VO_BORDER + w].cpu().numpy()

@@ -83,9 +83,7 @@ def test_pyramid_scharr_sizes(engine_factory, W, H):
             assert np.array_equal(eng.pyramid_level(1, lv, b), ref), f"b={b} pyramid level {lv}"
             w, h, p, o = d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv]
             n = (h + 2 * Bd) * p
-            t = eng.t["der1"][b]
-            full = torch.stack([t[q * d.pyr_stride + o:q * d.pyr_stride + o + n].view(h + 2 * Bd, p)
-                                for q in (0, 1)], dim=-1).cpu().numpy()
+            full = eng.t["der1"][b].view(-1, 2)[o:o + n].view(h + 2 * Bd, p, 2).cpu().numpy()
             assert np.array_equal(full[Bd:Bd + h, Bd:Bd + w], O.scharr(ref)), f"b={b} scharr level {lv}"
             inner = np.zeros(full.shape[:2], bool)
             inner[Bd:Bd + h, Bd:Bd + w] = True
