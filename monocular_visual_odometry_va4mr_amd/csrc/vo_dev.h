@@ -169,3 +169,16 @@ VO_DEV uint32_t rng_next(uint64_t& s)
 }
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+// host: compute units of the current device, cached per device id (launch-shape decisions of
+// the C ABI entry points; a benign race only stores the same value twice)
+static inline int device_cus()
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    static int cache[64] = {0};
+    if (dev < 64 && cache[dev] > 0) return cache[dev];
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (dev < 64) cache[dev] = n;
+    return n;
+}

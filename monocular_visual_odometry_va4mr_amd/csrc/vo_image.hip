@@ -608,13 +608,10 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // may run up to 3 bytes past a row end (next row, or the >= 64-byte tail slack that the
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
-// WPB waves per block work as WPB independent one-wave blocks (own LDS slice, virtual block
-// index blockIdx.x * WPB + wave): with WPB = 4 a finished block frees four wave slots at once,
-// so the other stream group's 4-wave kernels (PnP, triangulation) are not starved of a CU by a
-// flood of single-wave LK blocks (VO_LK_WPB)
-template <int WW, int WH, int WPB>
-__global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
+template <int WW, int WH>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
 {
+    constexpr int WPB = 1;
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
     constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
     constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
@@ -990,397 +987,6 @@ __global__ void __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(8
     }
     level = level_lo;
     LKPROF_SET(1, wall_clock64());
-}
-
-// ---------------------------------------------------------------------------------------
-// k_lk_h: k_lk_w<15,15>'s calcOpticalFlowPyrLK (same integer / float operation sequence, so
-// bit-exact with the CPU restatement) with TWO points per wave: lanes 0-31 carry one point and
-// lanes 32-63 another (a "half"), eight window pixels per lane.
-//
-// Why: k_lk_w is stall-bound at its 8 waves per SIMD (SQ_WAIT_INST_ANY 0.59 of wave
-// cycles, 0.49 of VALU issue), and about two thirds of an iteration's VALU work there is
-// wave-uniform -- weights, the 2x2 solve, the convergence tests, the DPP reductions -- which
-// all 64 lanes compute for one point.  Here the same instructions serve two points, the
-// reductions are 32-lane (row sums, one row_bcast:15, two readlanes), and per-half values
-// (estimate, weights, tensor) live in VGPRs, so the halves branch independently under the
-// exec mask (a finished half idles while the other iterates).
-//
-// LDS per half: the packed-quad J tile QT (2,304 B) and its raw rows JR (768 B); the I / dI
-// window rows IR / DR are staged into the QT space and consumed before QT is built from JR
-// (one memory round trip per level as before), so a wave holds 6 KB instead of 2 x 5.1 KB.
-// Window map of a half: column l % 16, rows 4(j/2) + j%2 + 2g (g = l / 16, j = 0..7): the two
-// 16-lane groups of a half read rows 48 dwords apart (banks 16 apart, conflict-free).
-__device__ __forceinline__ int lkh_pick(int x, bool hi)
-{
-    const int a = __builtin_amdgcn_readlane(x, 31), b = __builtin_amdgcn_readlane(x, 63);
-    return hi ? b : a;
-}
-#define LKH_DPP(v, ctl, rm) v += __builtin_amdgcn_update_dpp(0, v, ctl, rm, 0xF, false)
-// per-half int32 sums: row reductions, row_bcast:15 folds row 0 into row 1 and row 2 into
-// row 3, lanes 31 / 63 hold the two totals
-VO_DEV int lkh_sum(int x, bool hi)
-{
-    LKH_DPP(x, 0xB1, 0xF); LKH_DPP(x, 0x4E, 0xF); LKH_DPP(x, 0x124, 0xF); LKH_DPP(x, 0x128, 0xF);
-    LKH_DPP(x, 0x142, 0xA);
-    return lkh_pick(x, hi);
-}
-VO_DEV void lkh_sum2(int& x, int& y, bool hi)
-{
-    LKH_DPP(x, 0xB1, 0xF); LKH_DPP(y, 0xB1, 0xF); LKH_DPP(x, 0x4E, 0xF); LKH_DPP(y, 0x4E, 0xF);
-    LKH_DPP(x, 0x124, 0xF); LKH_DPP(y, 0x124, 0xF); LKH_DPP(x, 0x128, 0xF); LKH_DPP(y, 0x128, 0xF);
-    LKH_DPP(x, 0x142, 0xA); LKH_DPP(y, 0x142, 0xA);
-    x = lkh_pick(x, hi);
-    y = lkh_pick(y, hi);
-}
-VO_DEV void lkh_sum3(int& x, int& y, int& z, bool hi)
-{
-    LKH_DPP(x, 0xB1, 0xF); LKH_DPP(y, 0xB1, 0xF); LKH_DPP(z, 0xB1, 0xF);
-    LKH_DPP(x, 0x4E, 0xF); LKH_DPP(y, 0x4E, 0xF); LKH_DPP(z, 0x4E, 0xF);
-    LKH_DPP(x, 0x124, 0xF); LKH_DPP(y, 0x124, 0xF); LKH_DPP(z, 0x124, 0xF);
-    LKH_DPP(x, 0x128, 0xF); LKH_DPP(y, 0x128, 0xF); LKH_DPP(z, 0x128, 0xF);
-    LKH_DPP(x, 0x142, 0xA); LKH_DPP(y, 0x142, 0xA); LKH_DPP(z, 0x142, 0xA);
-    x = lkh_pick(x, hi);
-    y = lkh_pick(y, hi);
-    z = lkh_pick(z, hi);
-}
-#undef LKH_DPP
-// exact per-half sum of partials whose total may exceed 32 bits (p = hi16 * 2^16 + lo16)
-VO_DEV int64_t lkh_sum_split(int p, bool hi)
-{
-    int h16 = p >> 16, l16 = p & 0xFFFF;
-    lkh_sum2(h16, l16, hi);
-    return (int64_t)h16 * 65536 + (int64_t)l16;
-}
-
-__global__ void __launch_bounds__(64) k_lk_h(LKParams P, int level_hi, int level_lo, int B, int nb)
-{
-    constexpr int WW = 15, WH = 15, NPX = WW * WH, MAXJ = 8;
-    constexpr int TW = WW + 2 * LK_M, TH = WH + 2 * LK_M;
-    constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
-    constexpr int QM = (TW + 3) / 4, QS = 4 * QM;
-    constexpr int IRS = QS / 4, JRS = 8;
-    constexpr int IR_DW = (WH + 2) * IRS, DR_OFF = (IR_DW + 3) & ~3, DR_DW = (WH + 2) * QS;
-    static_assert(JRW >= QM + 1 && JRW <= JRS && IRW <= IRS && IRW <= 8 && DRW == 16 && QS % 4 == 0 && NPX <= 256,
-                  "k_lk_h staging layout");
-    static_assert(DR_OFF + DR_DW <= (TH + 1) * QM * 4, "I / dI rows must fit the QT space they alias");
-    static_assert((2 * QS) % 32 == 16, "k_lk_h window map: the 16-lane groups of a half read rows 2 apart");
-    __shared__ uint4 QT4_all[2][(TH + 1) * QM];
-    __shared__ uint32_t JR_all[2][(TH + 1) * JRS];
-    const int lane = lane_id();
-    const bool hi = lane >= 32;
-    const int h = hi ? 1 : 0, l = lane & 31;
-    uint4* QT4 = QT4_all[h];
-    const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
-    uint32_t* JR = JR_all[h];
-    uint32_t* IR = reinterpret_cast<uint32_t*>(QT4);          // aliases QT during the level setup
-    uint32_t* DR = IR + DR_OFF;
-    const uint8_t* ir8 = (const uint8_t*)IR;
-    int b, pb;
-    if (!lk_block(B, nb, b, pb, false)) return;
-    if (P.chain_status && P.chain_status[b] != 0) return;
-    const int n0 = P.n0 ? P.n0[b] : 0;
-    int n1 = P.n1 ? P.n1[b] : 0;
-    if (n1 <= P.seg1_min) n1 = 0;
-    const int ntot = n0 + n1;
-    const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
-    const int g = l >> 4, wcol = l & 15;
-    const int toff0 = 2 * g * QS + wcol;
-    int toff[MAXJ];
-#pragma unroll
-    for (int j = 0; j < MAXJ; ++j) toff[j] = toff0 + (4 * (j >> 1) + (j & 1)) * QS;
-    // pixel j of this lane is inside the window (column 15 and row 15 are dead lanes); kept as
-    // a function of (wcol, g) rather than eight lane masks held in SGPRs
-    auto live = [&](int j) { return wcol < WW && (j != MAXJ - 1 || g == 0); };
-    int tx0 = 0, ty0 = 0, jsh = 0;
-    int cols = 0, rows = 0, pitch = 0, loff = 0;
-    const __amdgpu_buffer_rsrc_t rI = lkq_rsrc(P.prev + (int64_t)b * P.pstride, P.pstride);
-    const __amdgpu_buffer_rsrc_t rJ = lkq_rsrc(P.next + (int64_t)b * P.pstride, P.pstride);
-    const __amdgpu_buffer_rsrc_t rD = lkq_rsrc(P.der + (int64_t)b * P.dstride, 2 * P.dstride);
-    constexpr int NIR = ((WH + 1) * 8 + 31) / 32, NDR = ((WH + 1) * 16 + 31) / 32;
-    constexpr int NJR = ((TH + 1) * JRS + 31) / 32, NQT = (TH * QM + 31) / 32;
-    static_assert(NJR * 32 == (TH + 1) * JRS, "k_lk_h J rows: every staging lane loads");
-    auto j_origin = [&](int inx, int iny) {
-        tx0 = max(inx - LK_M, -VO_BORDER);
-        ty0 = min(max(iny - LK_M, -VO_BORDER), rows + VO_BORDER - 1 - TH);
-        jsh = (tx0 + VO_BORDER) & 3;
-    };
-    auto j_issue = [&](uint32_t (&v)[NJR]) {
-        const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
-        const int ln = l + opaque0();
-        const int vo = loff + gy0 * pitch + (gx0 & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);
-#pragma unroll
-        for (int k = 0; k < NJR; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, vo, 4 * k * pitch, 0);
-    };
-    // JR rows -> LDS, then the packed 2x2 quads QT (as k_lk_w's j_store)
-    auto j_store = [&](const uint32_t (&v)[NJR]) {
-#pragma unroll
-        for (int k = 0; k < NJR; ++k) JR[l + 32 * k] = v[k];
-        wave_lds_sync();
-        const int ln = l + opaque0();
-#pragma unroll
-        for (int k = 0; k < NQT; ++k) {
-            const int q = ln + 32 * k;
-            if (q < TH * QM) {
-                const int r = q / QM, m = q - r * QM;
-                const uint32_t* j0 = JR + r * JRS + m;
-                const uint32_t a0 = j0[0], a1 = j0[1], b0 = j0[JRS], b1 = j0[JRS + 1];
-                const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
-                const uint32_t Bv = jsh == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, jsh + 1);
-                const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
-                const uint32_t D = jsh == 3 ? b1 : __builtin_amdgcn_alignbyte(b1, b0, jsh + 1);
-                const uint32_t X = __builtin_amdgcn_perm(Bv, A, 0x05010400u), Y = __builtin_amdgcn_perm(Bv, A, 0x07030602u);
-                const uint32_t Xp = __builtin_amdgcn_perm(D, C, 0x05010400u), Yp = __builtin_amdgcn_perm(D, C, 0x07030602u);
-                QT4[q] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
-                                    __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
-            }
-        }
-        wave_lds_sync();
-    };
-    auto stage_j = [&](int inx, int iny) {
-        j_origin(inx, iny);
-        uint32_t v[NJR];
-        j_issue(v);
-        wave_lds_sync();
-        j_store(v);
-    };
-    // the four bilinear weights, split into the 7-bit halves the two unsigned dots take; w11
-    // can be -1: it enters as w11 + neg and the dot result is corrected by the J11 tap
-    auto weights = [&](float aa, float bb, uint32_t& wlo, uint32_t& whi, int& neg) {
-        const int w00 = __float2int_rn((1.f - aa) * (1.f - bb) * (float)(1 << 14));
-        const int w01 = __float2int_rn(aa * (1.f - bb) * (float)(1 << 14));
-        const int w10 = __float2int_rn((1.f - aa) * bb * (float)(1 << 14));
-        const int w11 = (1 << 14) - w00 - w01 - w10;
-        neg = w11 < 0;
-        wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
-        whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
-    };
-    const float FLT_SCALE = 1.f / (1 << 20);
-    // points 2 s + h for s = pb, pb + nb, ...: the halves of a wave take neighbouring points
-    for (int s = pb; 2 * s + h < ntot; s += nb) {
-        const int p = 2 * s + h;
-        const float* src = (p < n0) ? (P.p0 + ((int64_t)b * P.cap0 + p) * 2) : (P.p1 + ((int64_t)b * P.cap1 + (p - n0)) * 2);
-        const int64_t oidx = (int64_t)b * P.ocap + p;
-        const float ptx = src[0], pty = src[1];
-        int status = 1;
-        float errv = 0.f;
-        float ox = 0.f, oy = 0.f;
-        for (int level = level_hi; level >= level_lo; --level) {
-            cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level]; loff = (int)P.loff[level];
-            const float sc = __builtin_ldexpf(1.f, -level);
-            float px = ptx * sc, py = pty * sc;
-            if (level == P.L) { ox = px; oy = py; }
-            else if (level == level_hi) { ox = P.out[2 * oidx] * 2.f; oy = P.out[2 * oidx + 1] * 2.f; }
-            else { ox *= 2.f; oy *= 2.f; }
-            px -= hx;
-            py -= hy;
-            const int ipx = (int)floorf(px), ipy = (int)floorf(py);
-            if (ipx < -WW || ipx >= cols || ipy < -WH || ipy >= rows) {
-                if (level == 0) { status = 0; errv = 0.f; }
-                continue;
-            }
-            bool staged = false;
-            // the level's I window and dI as int16 pairs of neighbouring pixels (2j, 2j + 1):
-            // |I * 32| <= 8160 and |dI| <= 4080 fit, and v_dot2_i32_i16 forms the window sums
-            // of two pixels at once (half the registers of one int per pixel)
-            constexpr int NP = MAXJ / 2;
-            uint32_t ip[NP], ixp[NP], iyp[NP];
-            float A11, A12, A22, D;
-            {
-                const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
-                const int ish = gx & 3;
-                const int ln = l + opaque0();
-                const int vi = loff + gy * pitch + (gx & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);
-                const int vd = 4 * (loff + gy * pitch + gx + (ln >> 4) * pitch + (ln & 15));
-                uint32_t vir[NIR], vdd[NDR], vjr[NJR];
-#pragma unroll
-                for (int k = 0; k < NIR; ++k) vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, vi, 4 * k * pitch, 0);
-#pragma unroll
-                for (int k = 0; k < NDR; ++k) vdd[k] = __builtin_amdgcn_raw_buffer_load_b32(rD, vd, 8 * k * pitch, 0);
-                {
-                    const int jx = (int)floorf(ox - hx), jy = (int)floorf(oy - hy);
-                    staged = !(jx < -WW || jx >= cols || jy < -WH || jy >= rows) && P.max_count > 0;
-                    if (staged) {
-                        j_origin(jx, jy);
-                        j_issue(vjr);
-                    }
-                }
-                wave_lds_sync();
-#pragma unroll
-                for (int k = 0; k < NIR; ++k) {
-                    const int r = (ln >> 3) + 4 * k, c = ln & 7;
-                    if (c < IRS) IR[r * IRS + c] = vir[k];
-                }
-#pragma unroll
-                for (int k = 0; k < NDR; ++k) {
-                    const int r = (ln >> 4) + 2 * k, c = ln & 15;
-                    DR[r * QS + c] = vdd[k];
-                }
-                wave_lds_sync();
-                float a = px - ipx, bb = py - ipy;
-                const int iw00 = __float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14));
-                const int iw01 = __float2int_rn(a * (1.f - bb) * (float)(1 << 14));
-                const int iw10 = __float2int_rn((1.f - a) * bb * (float)(1 << 14));
-                const int iw11 = (1 << 14) - iw00 - iw01 - iw10;
-                int ivl[MAXJ], gxl[MAXJ], gyl[MAXJ];
-                const v2i16 wp0 = as_v2i16((uint32_t)(iw00 & 0xffff) | ((uint32_t)iw01 << 16));
-                const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
-#pragma unroll
-                for (int j = 0; j < MAXJ; ++j) {
-                    const uint8_t* sp = ir8 + toff[j] + ish;
-                    const uint32_t* d = DR + toff[j];
-                    const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
-                    const int v = DESCALE(__mul24((int)sp[0], iw00) + __mul24((int)sp[1], iw01) +
-                                          __mul24((int)sp[QS], iw10) + __mul24((int)sp[QS + 1], iw11), 9);
-                    const int gx2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x05040100u)), wp1,
-                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x05040100u)), wp0,
-                                                               1 << 13, false), false) >> 14;
-                    const int gy2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x07060302u)), wp1,
-                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x07060302u)), wp0,
-                                                               1 << 13, false), false) >> 14;
-                    ivl[j] = live(j) ? v : 0;
-                    gxl[j] = live(j) ? gx2 : 0;
-                    gyl[j] = live(j) ? gy2 : 0;
-                }
-                int a11 = 0, a12 = 0, a22 = 0;
-#pragma unroll
-                for (int k = 0; k < NP; ++k) {
-                    ip[k] = ((uint32_t)ivl[2 * k] & 0xffffu) | ((uint32_t)ivl[2 * k + 1] << 16);
-                    ixp[k] = ((uint32_t)gxl[2 * k] & 0xffffu) | ((uint32_t)gxl[2 * k + 1] << 16);
-                    iyp[k] = ((uint32_t)gyl[2 * k] & 0xffffu) | ((uint32_t)gyl[2 * k + 1] << 16);
-                    a11 = __builtin_amdgcn_sdot2(as_v2i16(ixp[k]), as_v2i16(ixp[k]), a11, false);
-                    a12 = __builtin_amdgcn_sdot2(as_v2i16(ixp[k]), as_v2i16(iyp[k]), a12, false);
-                    a22 = __builtin_amdgcn_sdot2(as_v2i16(iyp[k]), as_v2i16(iyp[k]), a22, false);
-                }
-                // exact 32-bit per-half sums unless a lane's partial could overflow one
-                const bool twide = __ballot((uint32_t)a11 >= (1u << 26) || (uint32_t)a22 >= (1u << 26) ||
-                                            (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
-                wave_lds_sync();                 // I / dI reads done before QT (same space) is built
-                if (staged) j_store(vjr);
-                if (!twide) {
-                    lkh_sum3(a11, a12, a22, hi);
-                    A11 = (float)a11 * FLT_SCALE; A12 = (float)a12 * FLT_SCALE; A22 = (float)a22 * FLT_SCALE;
-                } else {
-                    A11 = (float)lkh_sum_split(a11, hi) * FLT_SCALE; A12 = (float)lkh_sum_split(a12, hi) * FLT_SCALE;
-                    A22 = (float)lkh_sum_split(a22, hi) * FLT_SCALE;
-                }
-                D = A11 * A22 - A12 * A12;
-                const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
-                if (minEig < P.min_eig || D < FLT_EPSILON) {
-                    if (level == 0) status = 0;
-                    continue;
-                }
-                D = 1.f / D;
-            }
-            float nx = ox - hx, ny = oy - hy;
-            float pdx = 0.f, pdy = 0.f;
-            bool lost = false;
-            for (int it = 0; it < P.max_count; ++it) {
-                const int inx = (int)floorf(nx), iny = (int)floorf(ny);
-                if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
-                    lost = true;
-                    break;
-                }
-                if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) {
-                    stage_j(inx, iny);
-                    staged = true;
-                }
-                uint32_t wlo, whi;
-                int neg;
-                weights(nx - inx, ny - iny, wlo, whi, neg);
-                const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
-                uint32_t qv[MAXJ];
-#pragma unroll
-                for (int j = 0; j < MAXJ; ++j) qv[j] = tb[toff[j]];
-                int b1 = 0, b2 = 0;
-                const uint32_t nmask = neg ? 0xFFu : 0u;
-                // the w11 = -1 correction only in its own (wave-uniform) copy of the loop
-                auto mismatch = [&](auto negc) {
-                    // the correcting copy takes its weights through an opaque move, so the
-                    // compiler cannot hoist the dots of both copies above the branch (that held
-                    // all sixteen dot results at once)
-                    const uint32_t wl = decltype(negc)::value ? wlo + opaque0() : wlo;
-                    const uint32_t wh = decltype(negc)::value ? whi + opaque0() : whi;
-#pragma unroll
-                    for (int k = 0; k < NP; ++k) {
-                        // DESCALE(J bilinear, 9) of the pixel pair (0 < sum < 2^22), packed as
-                        // int16 and minus the packed I window: the pair's diffs, then both
-                        // pixels' diff * dI terms in one v_dot2_i32_i16 per sum
-                        uint32_t s0 = (__builtin_amdgcn_udot4(qv[2 * k], wh, 0u, false) << 7) +
-                                      __builtin_amdgcn_udot4(qv[2 * k], wl, 256u, false);
-                        uint32_t s1 = (__builtin_amdgcn_udot4(qv[2 * k + 1], wh, 0u, false) << 7) +
-                                      __builtin_amdgcn_udot4(qv[2 * k + 1], wl, 256u, false);
-                        if (decltype(negc)::value) {
-                            s0 -= (qv[2 * k] >> 24) & nmask;
-                            s1 -= (qv[2 * k + 1] >> 24) & nmask;
-                        }
-                        const uint32_t jp = ((s1 << 7) & 0xffff0000u) | (s0 >> 9);
-                        const v2i16 dp = as_v2i16(jp) - as_v2i16(ip[k]);
-                        b1 = __builtin_amdgcn_sdot2(dp, as_v2i16(ixp[k]), b1, false);
-                        b2 = __builtin_amdgcn_sdot2(dp, as_v2i16(iyp[k]), b2, false);
-                    }
-                };
-                if (__ballot(neg) != 0) mismatch(std::true_type());
-                else mismatch(std::false_type());
-                const bool wide = __ballot((uint32_t)(b1 + (1 << 25)) >= (1u << 26) ||
-                                           (uint32_t)(b2 + (1 << 25)) >= (1u << 26)) != 0;
-                float fb1, fb2;
-                if (!wide) { lkh_sum2(b1, b2, hi); fb1 = (float)b1 * FLT_SCALE; fb2 = (float)b2 * FLT_SCALE; }
-                else { fb1 = (float)lkh_sum_split(b1, hi) * FLT_SCALE; fb2 = (float)lkh_sum_split(b2, hi) * FLT_SCALE; }
-                const float ddx = (A12 * fb2 - A22 * fb1) * D;
-                const float ddy = (A12 * fb1 - A11 * fb2) * D;
-                nx += ddx;
-                ny += ddy;
-                ox = nx + hx;
-                oy = ny + hy;
-                if ((double)ddx * ddx + (double)ddy * ddy <= P.eps2) break;
-                if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
-                    ox -= ddx * 0.5f;
-                    oy -= ddy * 0.5f;
-                    break;
-                }
-                pdx = ddx;
-                pdy = ddy;
-            }
-            if (lost) {
-                if (level == 0) status = 0;
-                continue;
-            }
-            if (status && level == 0) {
-                const float fx = ox - hx, fy = oy - hy;
-                const int inx = (int)floorf(fx), iny = (int)floorf(fy);
-                if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
-                    status = 0;
-                    continue;
-                }
-                if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) stage_j(inx, iny);
-                uint32_t wlo, whi;
-                int neg;
-                weights(fx - inx, fy - iny, wlo, whi, neg);
-                const uint32_t nmask = neg ? 0xFFu : 0u;
-                const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
-                int es = 0;
-#pragma unroll
-                for (int j = 0; j < MAXJ; ++j) {
-                    const uint32_t q = tb[toff[j]];
-                    uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
-                                   __builtin_amdgcn_udot4(q, wlo, 256u, false);
-                    sum -= (q >> 24) & nmask;
-                    const int ivj = (int)(int16_t)(ip[j >> 1] >> (16 * (j & 1)));
-                    const int diff = (int)(sum >> 9) - ivj;
-                    es += live(j) ? (diff < 0 ? -diff : diff) : 0;
-                }
-                errv = (float)lkh_sum(es, hi) / (float)(32 * WW * WH);
-            }
-        }   // levels
-        if (l == 0) {
-            P.out[2 * oidx] = ox;
-            P.out[2 * oidx + 1] = oy;
-            if (level_lo == 0) {
-                P.st[oidx] = (uint8_t)status;
-                if (P.err) P.err[oidx] = errv;
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------- tracking compaction (:282-290)
@@ -2390,20 +1996,12 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     // 0 in registers) unless VO_LK_FUSED=0: a level's launch lasts as long as its slowest
     // point (up to max_count iterations), so separate launches pay that tail once per level.
     static const int fused_env = [] { const char* e = getenv("VO_LK_FUSED"); return e ? atoi(e) : 1; }();
-    // two points per wave (k_lk_h) unless VO_LK_HALF=0: the same 2048 point slots per chain
-    // in 1024 one-wave blocks
-    static const int half_env = [] { const char* e = getenv("VO_LK_HALF"); return e ? atoi(e) : 1; }();
-    if (staged15 && fused_env && half_env) {
-        const int nbh = nb_env > 0 ? nb_env : 1024;
-        hipLaunchKernelGGL(k_lk_h, dim3(B * nbh), dim3(64), 0, st, P, L, 0, B, nbh);
-        return hip_ok() ? VO_OK : VO_EHIP;
-    }
     if (staged15 && fused_env) {
-        hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
+        hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {
-        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15, 1>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
+        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
         else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
         else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }

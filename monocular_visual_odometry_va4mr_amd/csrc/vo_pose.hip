@@ -682,7 +682,8 @@ __global__ void __launch_bounds__(256) k_pnp_apply(vo_dims d, vo_state s, const 
 #ifndef VO_PNP_WPE
 #define VO_PNP_WPE 2
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VO_PNP_WPE, 8)))
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 k_pnp_fused(PnPArgs A, vo_dims d, vo_state s)
 {
     pnp_ransac_block(A);
@@ -1066,8 +1067,11 @@ extern "C" int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_
     if (split == 1) {                     // the two-launch form (A/B measurements)
         hipLaunchKernelGGL(k_pnp_ransac, dim3(d->B), dim3(256), 0, st, P);
         hipLaunchKernelGGL(k_pnp_apply, dim3(d->B), dim3(256), 0, st, *d, *s, P.rvec, P.tvec, P.success, P.mask);
+    } else if (d->B > (device_cus() > 0 ? device_cus() : 256)) {
+        // more chains than CUs: two blocks per CU (as vo_pnp_triangulate)
+        hipLaunchKernelGGL(k_pnp_fused<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, st, P, *d, *s);
     } else {
-        hipLaunchKernelGGL(k_pnp_fused, dim3(d->B), dim3(256), 0, st, P, *d, *s);
+        hipLaunchKernelGGL(k_pnp_fused<1>, dim3(d->B), dim3(256), 0, st, P, *d, *s);
     }
     return hip_rc();
 }
@@ -1103,12 +1107,7 @@ extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_s
     fill_tri(T, d, o, s, 0);
     // more chains than CUs: the 2-waves/SIMD build (two blocks per CU, some registers spilled);
     // otherwise every block has a CU of its own and the unconstrained build is faster
-    static const int n_cu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 256;
-        return n;
-    }();
+    const int n_cu = device_cus() > 0 ? device_cus() : 256;      // of the current device
     if (d->B > n_cu) hipLaunchKernelGGL(k_pnp_tri<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     else hipLaunchKernelGGL(k_pnp_tri<1>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     return hip_rc();
