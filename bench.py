@@ -53,6 +53,7 @@ from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E
 SEQ_LEN = 4541          # KITTI seq00 frame count
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
 MFMA_PEAK_TF = 2500.0   # dense bf16 MFMA (no sparsity)
+MFMA_PEAK_I8 = 5000.0   # dense int8 MFMA: 32x32x32 in the cycles of bf16 32x32x16 (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -134,8 +135,9 @@ def sift_match_leg(device, preset, seed, n_frames, nfeatures=0, iters=2):
     """Detect + describe `n_frames` consecutive synthetic frames in ONE vo_sift_batch launch
     sequence, then match the n_frames - 1 consecutive pairs in ONE vo_bf_knn2_batch launch
     (BFMatcher.knnMatch k=2 on MFMA), each timed with HIP events on the current stream.
-    Rooflines: SIFT against HBM (sift_bytes per image), BF against the dense bf16 MFMA peak
-    (2 * nq * nt * 128 FLOP per pair on the real descriptor counts)."""
+    Rooflines: SIFT against HBM (sift_bytes per image), BF against the dense int8 MFMA peak
+    (2 * nq * nt * 128 integer ops per pair on the real descriptor counts; the bf16 peak when
+    VO_BF_BF16=1 selects the bf16 kernel)."""
     from monocular_visual_odometry_va4mr_amd.features import Sift, bf_knn2_batch
     rend = Renderer(preset, seed=seed, device=device)
     Rs, cs = poses(n_frames, rend.p)
@@ -173,9 +175,17 @@ def sift_match_leg(device, preset, seed, n_frames, nfeatures=0, iters=2):
             "sift_roofline": {"bound": "hbm", "kernel": "vo_sift_batch", "achieved": round(gbs, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
                               "algorithmic_bytes_per_image": sift_bytes(sift)},
-            "bf_roofline": {"bound": "mfma", "kernel": "vo_bf_knn2_batch", "achieved": round(tf, 2),
-                            "peak": MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TF, 4),
-                            "flop_per_launch": flop}}
+            "bf_roofline": bf_roofline(tf, flop)}
+
+
+def bf_roofline(tops, ops):
+    if os.environ.get("VO_BF_BF16") == "1":
+        return {"bound": "mfma", "kernel": "vo_bf_knn2_batch (k_bf_mfma, bf16)", "achieved": round(tops, 2),
+                "peak": MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(tops / MFMA_PEAK_TF, 4),
+                "flop_per_launch": ops}
+    return {"bound": "mfma", "kernel": "vo_bf_knn2_batch (k_bf_i8, int8)", "achieved": round(tops, 2),
+            "peak": MFMA_PEAK_I8, "unit": "TOP/s", "frac": round(tops / MFMA_PEAK_I8, 4),
+            "flop_per_launch": ops}
 
 
 def c3_leg(device, n_pairs=16, iters=2):

@@ -2,19 +2,24 @@
 // /root/reference/VisualOdometryPipeLine.py:36,229; SURVEY.md §8a row a4, §8d "BF kNN").
 //
 // B independent (query set, train set) problems per launch.  SIFT descriptors hold integers
-// 0..255, so bf16 operands and fp32 accumulation are exact (sum <= 128 * 255^2 < 2^24) and
-// the distances are those of OpenCV's float path bit for bit.
+// 0..255, so the squared distances are exact integers and OpenCV's float path (sum < 2^24,
+// then sqrtf) is reproduced bit for bit from them.
 //
-//  k_bf_prep   descriptors -> bf16 rows + integer squared norms (one wave per row)
-//  k_bf_mfma   block = 4 waves x 32 queries; 64-row train tiles double-buffered in LDS (16-B
-//              slots XOR-swizzled by row: conflict-free ds_read_b128); per 32-row sub-tile each
-//              wave runs 9 v_mfma_f32_32x32x16_bf16 with the TRAIN rows as the A operand and its
-//              queries as B, so every lane owns one query column and 16 train rows of the tile;
-//              the ninth K-step folds |t|^2 in, so the accumulator is s = 2 q.t - |t|^2 exactly.
-//              The lane keeps a running top-2 of s (= |q|^2 - d^2, |q|^2 constant per lane) with
-//              strict '>' in increasing train index, i.e. the (distance, index) order OpenCV's
-//              knnMatch produces; a per-lane max over the 16 candidates skips the insertion
-//              when none can enter.
+// Default path, int8 (v_mfma_i32_32x32x32_i8, twice the bf16 rate):
+//  k_bf_prep_i8  descriptors -> int8 rows v - 128 + centred squared norms |v'|^2.  The
+//                distance is shift-invariant: |q - t|^2 = |q'|^2 + |t'|^2 - 2 q'.t'.
+//  k_bf_i8       block = 4 waves x 32 queries; 128-row train tiles double-buffered in LDS,
+//                prefetched one tile ahead with buffer loads; per 32-row sub-tile each wave runs
+//                4 MFMAs (train rows = A, its queries = B), the next sub-tile's MFMAs issued
+//                before this one's epilogue.  Each lane owns one query and 16 train rows; it
+//                forms keys 16 s + (15 - reg) with s = 2 q'.t' - |t'|^2 = |q'|^2 - d^2 (one
+//                v_lshl_add per candidate, the norm term staged in LDS), takes the sub-tile's
+//                two largest keys (v_med3 / v_max chains) and inserts them into its running
+//                top-2: the (distance, index) order OpenCV's knnMatch produces.
+// Cross-check path, bf16 (VO_BF_BF16=1, identical results):
+//  k_bf_prep / k_bf_mfma  bf16 rows, 9 v_mfma_f32_32x32x16_bf16 per sub-tile (the ninth K-step
+//                folds |t|^2 in), running top-2 of s with strict '>' in increasing train index.
+// Both:
 //  k_bf_merge  merges the train splits (grid filling for small batches) and writes
 //              idx2 / dist2 = sqrtf(d2) (correctly rounded, as OpenCV's sqrt).
 //  k_bf_fixup  integer order equals float order only while sqrtf separates the integers
@@ -32,12 +37,15 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define BF_QB 128          // queries per block
-#define BF_TT 64           // train rows per LDS tile
+#define BF_TT 64           // train rows per LDS tile (bf16 kernel)
+#define BFI_TT 128         // train rows per LDS tile (int8 kernel; measured: 64 rows 12 % slower)
 #define BF_MAXSPLIT 16
 #define BF_SAFE (1 << 22)  // below this, distinct integer d2 have distinct sqrtf
 
 struct BfArgs {
     int B, qcap, tcap, tsplit;
+    int tt;                // train rows per tile of the launched kernel (splits are multiples)
+    int qb;                // queries per block
     const __bf16* qbf;     // [B][qcap][128]
     const __bf16* tbf;     // [B][tcap][128]
     const int32_t* qn;     // [B][qcap] |q|^2
@@ -50,6 +58,9 @@ struct BfArgs {
     int32_t* flag_n;       // fixup list length
     int32_t* flag_list;    // [B * qcap] b * qcap + q
 };
+
+// train rows per split of a problem with nt rows (a multiple of the tile rows)
+VO_DEV int bf_per(int nt, const BfArgs& A) { return (((nt + A.tsplit - 1) / A.tsplit) + A.tt - 1) / A.tt * A.tt; }
 
 // (d, i) lexicographic order; absent entries are (INT_MAX, -1) and never precede a real one
 VO_DEV bool lex_lt(int da, int ia, int db, int ib) { return da < db || (da == db && (unsigned)ia < (unsigned)ib); }
@@ -96,16 +107,16 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 {
     __shared__ uint4 tile[2][BF_TT * 16];
     __shared__ uint4 tnp[2][BF_TT * 2];          // norm bytes (k = 128..135) | zeros (136..143)
-    const int nqb = (A.qcap + BF_QB - 1) / BF_QB;
+    const int nqb = (A.qcap + A.qb - 1) / A.qb;
     int blk = blockIdx.x;
     const int sp = blk % A.tsplit;
     blk /= A.tsplit;
     const int qb = blk % nqb, b = blk / nqb;
     if (b >= A.B) return;
     const int nq = A.nq[b], nt = A.nt[b];
-    const int q0 = qb * BF_QB;
+    const int q0 = qb * A.qb;
     if (q0 >= nq) return;
-    const int per = (((nt + A.tsplit - 1) / A.tsplit) + BF_TT - 1) & ~(BF_TT - 1);
+    const int per = bf_per(nt, A);
     const int tlo = sp * per, thi = min(nt, tlo + per);
     const int ntile = thi > tlo ? (thi - tlo + BF_TT - 1) / BF_TT : 0;
     const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
@@ -201,13 +212,239 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
     if (h == 0 && qv) A.part[((int64_t)b * A.tsplit + sp) * A.qcap + qi] = make_int4(d0, i0, d1, i1);
 }
 
+// ---- i8 path (default).  Descriptors are integers 0..255, so v - 128 is an exact int8 and
+// |q - t|^2 = |q'|^2 + |t'|^2 - 2 q'.t' with q' = q - 128, t' = t - 128 (the distance is
+// shift-invariant); v_mfma_i32_32x32x32_i8 forms q'.t' exactly in int32 at twice the bf16 rate.
+// The lane keeps the running top-2 of s = 2 q'.t' - |t'|^2 (= |q'|^2 - d^2), as k_bf_mfma does.
+// With |t'|^2 = 2h + p (p = parity) the MFMA accumulator starts at -h, so it ends at
+// a = q'.t' - h and s = 2a - p: s orders as (a descending, p ascending), every s <= 2a, and the
+// per-candidate work is one v_max3 per two candidates plus one test against the lane's
+// second-best; only candidates that may enter (2 max(a) > s1, rare) form s exactly.
+//
+//  k_bf_prep_i8  descriptors -> int8 rows (v - 128) + centered squared norms |v'|^2; eight
+//                threads per row, 16 values each (four float4 loads, one 16-byte store)
+//  k_bf_i8       block = 4 waves x 32 queries; 64-row int8 train tiles double-buffered in LDS
+//                (16-B slots XOR-swizzled by row); per tile each wave runs 2 x 4 MFMAs (two
+//                32-row sub-tiles, interleaved) with the train rows as A and its queries as B.
+//                Lane (r, g) supplies bytes 16g..16g+15 of every 32-byte K chunk for both
+//                operands: the same k for the same (g, element) on both sides, so the MFMA sums
+//                every k of the chunk once whatever the hardware's k order inside a chunk.
+__global__ void __launch_bounds__(256) k_bf_prep_i8(const float* __restrict__ src, const int32_t* n, int B, int cap,
+                                                    int8_t* __restrict__ dst, int32_t* __restrict__ nrm)
+{
+    const int row = blockIdx.x * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+    const int b = row / cap, r = row - b * cap;
+    const bool ok = b < B && r < n[min(b, B - 1)];
+    int ss = 0;
+    if (ok) {
+        const float4* s4 = reinterpret_cast<const float4*>(src + (int64_t)row * 128 + 16 * part);
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 v = s4[k];
+            const int a0 = (int)v.x - 128, a1 = (int)v.y - 128, a2 = (int)v.z - 128, a3 = (int)v.w - 128;
+            ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+            w[k] = (uint32_t)(a0 & 255) | ((uint32_t)(a1 & 255) << 8) | ((uint32_t)(a2 & 255) << 16) |
+                   ((uint32_t)(a3 & 255) << 24);
+        }
+        *reinterpret_cast<uint4*>(dst + (int64_t)row * 128 + 16 * part) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    ss += __shfl_xor(ss, 4, 64);
+    if (ok && part == 0) nrm[row] = ss;
+}
+
+// middle of three (v_med3_i32): with hi >= lo, med3(hi, lo, v) = max(lo, min(hi, v))
+VO_DEV int med3_i32(int a, int b, int c)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+#define BFI_FLOOR (-(1 << 25))      // below every real s = 2 q'.t' - |t'|^2 >= -3 * 2^21
+#define BFI_ABSENT_KEY (-(1 << 30)) // staged key term of absent train rows: s <= -2^26 < BFI_FLOOR
+
+// TT train rows per LDS tile, QG groups of 32 queries per wave (a train fragment read from LDS
+// feeds QG MFMAs; QG = 2 measured 30 % slower: 150 VGPRs, 3 waves per SIMD).  The vector unit,
+// not the matrix pipe, bounds this kernel: ~3 VALU instructions per (query, train) candidate
+// (key, v_med3, v_max) against 1/8 MFMA cycle.
+template <int TT, int QG>
+__global__ void __launch_bounds__(256) k_bf_i8(BfArgs A)
+{
+    static_assert(TT % 32 == 0 && TT <= 256, "tile rows");
+    constexpr int NPRE = TT * 8 / 256;            // 16-byte slots per thread per tile
+    __shared__ uint4 tile[2][TT * 8];             // TT rows x 128 B
+    __shared__ int ntn[2][TT];                    // -|t'|^2 per row
+    const int nqb = (A.qcap + A.qb - 1) / A.qb;
+    int blk = blockIdx.x;
+    const int sp = blk % A.tsplit;
+    blk /= A.tsplit;
+    const int qb = blk % nqb, b = blk / nqb;
+    if (b >= A.B) return;
+    const int nq = A.nq[b], nt = A.nt[b];
+    const int q0 = qb * A.qb;
+    if (q0 >= nq) return;
+    const int per = bf_per(nt, A);
+    const int tlo = sp * per, thi = min(nt, tlo + per);
+    const int ntile = thi > tlo ? (thi - tlo + TT - 1) / TT : 0;
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    const int h = lane >> 5, col = lane & 31;
+    const int8_t* qi8 = reinterpret_cast<const int8_t*>(A.qbf);
+    v4i qf[QG][4];
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+        const int qi = q0 + 32 * (QG * w + g) + col;
+        const int8_t* qrow = qi8 + ((int64_t)b * A.qcap + (qi < nq ? qi : q0)) * 128 + 16 * h;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[g][c] = *reinterpret_cast<const v4i*>(qrow + 32 * c);
+    }
+    // the split's rows through buffer resources sized to end at thi: rows past it read as
+    // zero (no per-row branch, so the prefetch stays in flight across the MFMAs)
+    const int8_t* Tb = reinterpret_cast<const int8_t*>(A.tbf) + ((int64_t)b * A.tcap + tlo) * 128;
+    const int32_t* TN = A.tn + (int64_t)b * A.tcap;
+    const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc((void*)Tb, (short)0, (thi - tlo) * 128, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rN =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(TN + tlo), (short)0, (thi - tlo) * 4, 0x00020000);
+    v4i pre[NPRE];
+    int pren = 0;
+    // loop-invariant per-lane offsets, tile offset in the scalar offset: no address VGPR that the
+    // MFMA results could be allocated over while a load is in flight
+    const int vT = tid * 16, vN = (tid & (TT - 1)) * 4;
+    auto gload = [&](int t0) {
+#pragma unroll
+        for (int i = 0; i < NPRE; ++i)
+            pre[i] = __builtin_amdgcn_raw_buffer_load_b128(rT, vT, (t0 - tlo) * 128 + 4096 * i, 0);
+        pren = __builtin_amdgcn_raw_buffer_load_b32(rN, vN, (t0 - tlo) * 4, 0);
+    };
+    // 16-byte slot j of row r lives at slot j ^ ((r >> 1) & 7): the 16 rows of a ds_read_b128
+    // lane group ({0-3,12-15,20-27} / {4-11,16-19,28-31}) then cover all 64 banks once
+    auto lstore = [&](int buf, int t0) {
+#pragma unroll
+        for (int i = 0; i < NPRE; ++i) {
+            const int e = tid + 256 * i, row = e >> 3, slot = e & 7;
+            tile[buf][row * 8 + (slot ^ ((row >> 1) & 7))] = make_uint4(pre[i].x, pre[i].y, pre[i].z, pre[i].w);
+        }
+        if (tid < TT) {
+            // key term of row tid: 16 (-|t'|^2) + (15 - reg), reg = the accumulator register that
+            // holds this row in the 32x32 C layout (row bits 0-1 = reg & 3, bits 3-4 = reg >> 2)
+            const int rl = tid & 31, reg = (rl & 3) | ((rl >> 3) << 2);
+            ntn[buf][tid] = t0 + tid < thi ? (-pren) * 16 + (15 - reg) : BFI_ABSENT_KEY;
+        }
+    };
+    int s0[QG], s1[QG], i0[QG], i1[QG], thr[QG];      // thr = 16 s1 + 15: key > thr <=> s > s1
+#pragma unroll
+    for (int g = 0; g < QG; ++g) { s0[g] = s1[g] = BFI_FLOOR; i0[g] = i1[g] = -1; thr[g] = 16 * BFI_FLOOR + 15; }
+    if (ntile > 0) {
+        gload(tlo);
+        lstore(0, tlo);
+    }
+    // every load so far complete on every path: otherwise the loop inherits "query fragments
+    // may be pending" from the ntile == 0 path and waits on the prefetch before each MFMA
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int k = 0; k < ntile; ++k) {
+        const int buf = k & 1, t0 = tlo + TT * k;
+        if (k + 1 < ntile) gload(t0 + TT);             // next tile in flight during the MFMAs
+        auto mfma_sub = [&](int sub, v16i* acc) {
+            const int row = sub * 32 + col;
+#pragma unroll
+            for (int g = 0; g < QG; ++g) acc[g] = v16i{};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint4 u = tile[buf][row * 8 + ((2 * c + h) ^ ((row >> 1) & 7))];
+                const v4i af = {(int)u.x, (int)u.y, (int)u.z, (int)u.w};
+#pragma unroll
+                for (int g = 0; g < QG; ++g)
+                    acc[g] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af, qf[g][c], acc[g], 0, 0, 0);
+            }
+        };
+        auto epilogue = [&](int sub, v16i* acc) {
+            // C layout: column = lane & 31 (query), row = (reg & 3) + 8 * (reg >> 2) + 4 * h (train).
+            // key = 32 q'.t' + 16 (-|t'|^2) + (15 - reg) = 16 s + (15 - reg): the largest key is the
+            // largest s, ties to the lowest register = the lowest train index of the lane
+            const int4* n4 = reinterpret_cast<const int4*>(&ntn[buf][sub * 32 + 4 * h]);
+            int4 nv[4];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) nv[g4] = n4[2 * g4];     // rows 8 g4 + 4h + 0..3
+            const int rbase = t0 + sub * 32 + 4 * h;
+#pragma unroll
+            for (int g = 0; g < QG; ++g) {
+                int kk[16];
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    kk[4 * g4 + 0] = (acc[g][4 * g4 + 0] << 5) + nv[g4].x;
+                    kk[4 * g4 + 1] = (acc[g][4 * g4 + 1] << 5) + nv[g4].y;
+                    kk[4 * g4 + 2] = (acc[g][4 * g4 + 2] << 5) + nv[g4].z;
+                    kk[4 * g4 + 3] = (acc[g][4 * g4 + 3] << 5) + nv[g4].w;
+                }
+                // the lane's two largest keys of the sub-tile (only they can enter its top-2; keys
+                // are distinct in the low bits): four running top-2 chains (v_med3 + v_max per
+                // key), merged pairwise (hi = max, lo = med3(a1, b1, max(a2, b2)))
+                int t1[4], t2[4];
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int* v = kk + 4 * q4;
+                    t1[q4] = max(v[0], v[1]);
+                    t2[q4] = min(v[0], v[1]);
+                    t2[q4] = med3_i32(t1[q4], t2[q4], v[2]);
+                    t1[q4] = max(t1[q4], v[2]);
+                    t2[q4] = med3_i32(t1[q4], t2[q4], v[3]);
+                    t1[q4] = max(t1[q4], v[3]);
+                }
+                const int u1 = max(t1[0], t1[1]), u2 = med3_i32(t1[0], t1[1], max(t2[0], t2[1]));
+                const int w1 = max(t1[2], t1[3]), w2 = med3_i32(t1[2], t1[3], max(t2[2], t2[3]));
+                const int m = max(u1, w1), m2 = med3_i32(u1, w1, max(u2, w2));
+                auto insert = [&](int key) {
+                    const int sv = key >> 4, reg = 15 - (key & 15);
+                    const int ix = rbase + (reg & 3) + 8 * (reg >> 2);
+                    const bool in = key > thr[g], c0 = sv > s0[g];
+                    s1[g] = in ? (c0 ? s0[g] : sv) : s1[g];
+                    i1[g] = in ? (c0 ? i0[g] : ix) : i1[g];
+                    s0[g] = in && c0 ? sv : s0[g];
+                    i0[g] = in && c0 ? ix : i0[g];
+                    thr[g] = 16 * s1[g] + 15;
+                };
+                insert(m);
+                if (__builtin_expect(m2 > thr[g], 0)) insert(m2);     // both entered somewhere in the wave
+            }
+        };
+        // software pipeline: the next sub-tile's MFMAs are issued before this one's epilogue, so
+        // the matrix pipe works while the vector unit forms keys and the top-2
+        v16i accA[QG], accB[QG];
+        mfma_sub(0, accA);
+#pragma unroll
+        for (int sub = 0; sub < TT / 32; ++sub) {
+            v16i* cur = (sub & 1) ? accB : accA;
+            v16i* nxt = (sub & 1) ? accA : accB;
+            if (sub + 1 < TT / 32) mfma_sub(sub + 1, nxt);
+            epilogue(sub, cur);
+        }
+        if (k + 1 < ntile) lstore(buf ^ 1, t0 + TT);
+        __syncthreads();
+    }
+    // d' = |t'|^2 - 2 q'.t' = -s (absent: INT_MAX); the two half-waves hold the same queries
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+        const int qi = q0 + 32 * (QG * w + g) + col;
+        int d0 = i0[g] >= 0 ? -s0[g] : INT_MAX, d1 = i1[g] >= 0 ? -s1[g] : INT_MAX;
+        int j0 = i0[g], j1 = i1[g];
+        merge2(d0, j0, d1, j1, __shfl_xor(d0, 32, 64), __shfl_xor(j0, 32, 64), __shfl_xor(d1, 32, 64),
+               __shfl_xor(j1, 32, 64));
+        if (h == 0 && qi < nq) A.part[((int64_t)b * A.tsplit + sp) * A.qcap + qi] = make_int4(d0, j0, d1, j1);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_bf_merge(BfArgs A)
 {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = row / A.qcap, q = row - b * A.qcap;
     if (b >= A.B || q >= A.nq[b]) return;
     int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
-    const int per = (((A.nt[b] + A.tsplit - 1) / A.tsplit) + BF_TT - 1) & ~(BF_TT - 1);
+    const int per = bf_per(A.nt[b], A);
     for (int sp = 0; sp < A.tsplit; ++sp) {
         if (sp * per >= A.nt[b]) break;            // empty split: its block never ran
         const int4 p = A.part[((int64_t)b * A.tsplit + sp) * A.qcap + q];
@@ -274,22 +511,25 @@ __global__ void __launch_bounds__(256) k_bf_fixup(BfArgs A, const float* __restr
 // ======================================================================= host side
 #define VO_STREAM(s) ((hipStream_t)(s))
 
-static int bf_tsplit(int B, int qcap, int tcap)
+static int bf_tsplit(int B, int qcap, int tcap, int qb, int tt)
 {
-    const int blocks = B * ((qcap + BF_QB - 1) / BF_QB);
+    const int blocks = B * ((qcap + qb - 1) / qb);
     int sp = (2048 + blocks - 1) / blocks;              // about 8 blocks per CU
-    const int tiles = (tcap + BF_TT - 1) / BF_TT;
+    const int tiles = (tcap + tt - 1) / tt;
     if (sp > tiles) sp = tiles;
     if (sp > BF_MAXSPLIT) sp = BF_MAXSPLIT;
     return sp < 1 ? 1 : sp;
 }
+
+// the most splits any kernel configuration below uses (sizes the partial-result scratch)
+static int bf_tsplit_max(int B, int qcap, int tcap) { return bf_tsplit(B, qcap, tcap, BF_QB, BF_TT); }
 
 static int64_t align256(int64_t v) { return (v + 255) & ~(int64_t)255; }
 
 extern "C" int64_t vo_bf_knn2_batch_scratch(int B, int32_t qcap, int32_t tcap)
 {
     if (B < 1 || qcap < 1 || tcap < 1) return -1;
-    const int sp = bf_tsplit(B, qcap, tcap);
+    const int sp = bf_tsplit_max(B, qcap, tcap);
     return align256((int64_t)B * qcap * 256) + align256((int64_t)B * tcap * 256) + align256((int64_t)B * qcap * 4) +
            align256((int64_t)B * tcap * 4) + align256((int64_t)B * sp * qcap * 16) + 256 + align256((int64_t)B * qcap * 4);
 }
@@ -303,7 +543,12 @@ extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_
     if (scratch_bytes < vo_bf_knn2_batch_scratch(B, qcap, tcap)) return VO_EARG;
     hipStream_t st = VO_STREAM(stream);
     BfArgs A;
-    A.B = B; A.qcap = qcap; A.tcap = tcap; A.tsplit = bf_tsplit(B, qcap, tcap);
+    // int8 MFMA path unless VO_BF_BF16=1 (the bf16 path; identical results, kept as its cross-check)
+    const char* bf16_env = getenv("VO_BF_BF16");
+    const bool use_bf16 = bf16_env && bf16_env[0] == '1';
+    const int tt = use_bf16 ? BF_TT : BFI_TT;
+    A.B = B; A.qcap = qcap; A.tcap = tcap; A.qb = BF_QB; A.tsplit = bf_tsplit(B, qcap, tcap, A.qb, tt);
+    A.tt = tt;
     char* p = (char*)scratch;
     A.qbf = (const __bf16*)p; p += align256((int64_t)B * qcap * 256);
     A.tbf = (const __bf16*)p; p += align256((int64_t)B * tcap * 256);
@@ -314,12 +559,20 @@ extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_
     A.flag_list = (int32_t*)p;
     A.nq = nq; A.nt = nt; A.idx2 = idx2; A.dist2 = dist2;
     if (hipMemsetAsync(A.flag_n, 0, sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
-    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap, 2.f,
-                       (__bf16*)A.qbf, (int32_t*)A.qn);
-    hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * tcap + 3) / 4), dim3(256), 0, st, t, nt, B, tcap, 1.f,
-                       (__bf16*)A.tbf, (int32_t*)A.tn);
-    const int nqb = (qcap + BF_QB - 1) / BF_QB;
-    hipLaunchKernelGGL(k_bf_mfma, dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
+    const int nqb = (qcap + A.qb - 1) / A.qb;
+    if (!use_bf16) {
+        hipLaunchKernelGGL(k_bf_prep_i8, dim3(((int64_t)B * qcap + 31) / 32), dim3(256), 0, st, q, nq, B, qcap,
+                           (int8_t*)A.qbf, (int32_t*)A.qn);
+        hipLaunchKernelGGL(k_bf_prep_i8, dim3(((int64_t)B * tcap + 31) / 32), dim3(256), 0, st, t, nt, B, tcap,
+                           (int8_t*)A.tbf, (int32_t*)A.tn);
+        hipLaunchKernelGGL((k_bf_i8<BFI_TT, 1>), dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
+    } else {
+        hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap, 2.f,
+                           (__bf16*)A.qbf, (int32_t*)A.qn);
+        hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * tcap + 3) / 4), dim3(256), 0, st, t, nt, B, tcap, 1.f,
+                           (__bf16*)A.tbf, (int32_t*)A.tn);
+        hipLaunchKernelGGL(k_bf_mfma, dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
+    }
     hipLaunchKernelGGL(k_bf_merge, dim3(((int64_t)B * qcap + 255) / 256), dim3(256), 0, st, A);
     hipLaunchKernelGGL(k_bf_fixup, dim3(64), dim3(256), 0, st, A, q, t);
     return hipGetLastError() == hipSuccess ? VO_OK : VO_EHIP;

@@ -26,6 +26,30 @@ def test_bf_knn2_exact():
                 assert dm.trainIdx == idx[i, j] and np.float32(dm.distance) == dist[i, j]
 
 
+def test_bf_knn2_i8_equals_bf16_at_c5_size(monkeypatch):
+    """The int8 MFMA kernel (default) and the bf16 one (VO_BF_BF16=1) at BASELINE C5's full
+    size, 2 x 8192 x 8192 with extreme (0/255-heavy) rows mixed in: identical indices and
+    distances -- a size-independent property where the C oracle would take minutes."""
+    from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    q = torch.randint(0, 256, (2, 8192, 128), generator=g).float()
+    t = torch.randint(0, 256, (2, 8192, 128), generator=g).float()
+    q[:, :64] = 255.0 * (q[:, :64] > 127)
+    t[:, :64] = 255.0 * (t[:, :64] < 128)
+    t[:, 100] = t[:, 99]
+    nq = torch.tensor([8192, 8000], dtype=torch.int32, device=dev)
+    nt = torch.tensor([8192, 7777], dtype=torch.int32, device=dev)
+    q, t = q.to(dev), t.to(dev)
+    monkeypatch.delenv("VO_BF_BF16", raising=False)
+    i8 = bf_knn2_batch(q, nq, t, nt)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("VO_BF_BF16", "1")
+    bf = bf_knn2_batch(q, nq, t, nt)
+    torch.cuda.synchronize()
+    assert torch.equal(i8[0], bf[0]) and torch.equal(i8[1], bf[1])
+
+
 def test_bf_knn2_batch_exact():
     """Batched MFMA matcher vs the C restatement: ragged / empty problems, an exact tie, and
     0/255 descriptors whose distances^2 pass 2^22 (the exact float-order fixup path)."""
