@@ -175,91 +175,111 @@ VO_DEV void svd_jacobi_wave(double* A, double* w, double* V)
     wave_lds_sync();
 }
 
+// f64 lane exchange inside groups of four lanes (DPP quad_perm): xor 1 / xor 2
+template <int CTRL>
+VO_DEV double dpp_quad_f64(double v)
+{
+    const int2 w = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, w.x, CTRL, 0xf, 0xf, false);
+    r.y = __builtin_amdgcn_update_dpp(0, w.y, CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, r);
+}
+VO_DEV double quad_sum_f64(double p)       // (p0 + p1) + (p2 + p3) in every lane of the quad
+{
+    const double s1 = p + dpp_quad_f64<0xB1>(p);      // quad_perm [1,0,3,2]
+    return s1 + dpp_quad_f64<0x4E>(s1);               // quad_perm [2,3,0,1]
+}
+
 // Round-robin Jacobi SVD (oracle/vo_oracle_geom.c svd_jacobi_rr) by one wave, A [M*N], w [N],
-// V [N*N] in LDS, N even.  Round r pairs the columns by the circle method; the N/2 pairs of a
-// round are disjoint.  Lane c < N keeps column c of A and of V in registers for all sweeps: per
-// round it fetches its partner's column with lane permutes, and both lanes of a pair form the
-// pair's sums in the scalar order, the same rotation, and each its own rotated column -- the
-// oracle's operations on the same values, so bit-identical, with no LDS traffic or wave
+// V [N*N] in LDS, N even, M a multiple of 4, 4 N <= 64.  Round r pairs the columns by the
+// circle method; the N/2 pairs of a round are disjoint.  Lane 4 c + q (c < N) keeps rows
+// q M/4 .. (q+1) M/4 - 1 of column c of A and of V in registers for all sweeps: per round it
+// fetches its partner column's quarter with lane permutes, forms its partial sums serially,
+// and the quad combines them as (p0 + p1) + (p2 + p3) -- the oracle's QUARTER_SUM; both
+// columns of a pair form the same sums, the same rotation, and each quarter its own rotated
+// rows: the oracle's operations on the same values, so bit-identical, with no LDS traffic or
 // barrier inside the sweeps.  (cs is unused; kept for the callers' LDS layout.)
 template <int M, int N>
 VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
 {
-    static_assert(N % 2 == 0 && N <= 64 && M <= 64, "round-robin SVD needs even N <= 64");
+    static_assert(N % 2 == 0 && 4 * N <= 64 && M % 4 == 0 && N % 4 == 0, "round-robin SVD shape");
     (void)cs;
-    constexpr int NP = N / 2;
+    constexpr int NP = N / 2, MQ = M / 4, NQ = N / 4;
     const int lane = lane_id();
-    const int col = lane < N ? lane : 0;
+    const bool act = lane < 4 * N;
+    const int col = act ? lane >> 2 : 0, q = lane & 3;
     // partner of this lane's column in every round
     int prt[N - 1];
 #pragma unroll
     for (int r = 0; r < N - 1; ++r) {
         prt[r] = col;
 #pragma unroll
-        for (int q = 0; q < NP; ++q) {
-            const int a = q == 0 ? 0 : ((q - 1 + r) % (N - 1)) + 1;
-            const int b = ((N - 2 - q + r) % (N - 1)) + 1;
+        for (int k = 0; k < NP; ++k) {
+            const int a = k == 0 ? 0 : ((k - 1 + r) % (N - 1)) + 1;
+            const int b = ((N - 2 - k + r) % (N - 1)) + 1;
             if (a == col) prt[r] = b;
             if (b == col) prt[r] = a;
         }
     }
-    double x[M], v[N];
+    double x[MQ], v[NQ];
 #pragma unroll
-    for (int k = 0; k < M; ++k) x[k] = A[k * N + col];
+    for (int k = 0; k < MQ; ++k) x[k] = A[(q * MQ + k) * N + col];
 #pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = k == col ? 1.0 : 0.0;
+    for (int k = 0; k < NQ; ++k) v[k] = q * NQ + k == col ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
         bool changed = false;
 #pragma unroll
         for (int r = 0; r < N - 1; ++r) {
             const int p = prt[r];
             const bool lo = col < p;           // this lane holds column i (= min of the pair)
-            double px[M], pv[N];
+            const int src = 4 * p + q;
+            double px[MQ], pv[NQ];
 #pragma unroll
-            for (int k = 0; k < M; ++k) px[k] = __shfl(x[k], p, 64);
+            for (int k = 0; k < MQ; ++k) px[k] = __shfl(x[k], src, 64);
 #pragma unroll
-            for (int k = 0; k < N; ++k) pv[k] = __shfl(v[k], p, 64);
-            double alpha = 0, beta = 0, gamma = 0;
+            for (int k = 0; k < NQ; ++k) pv[k] = __shfl(v[k], src, 64);
+            double pa = 0, pb = 0, pg = 0;
 #pragma unroll
-            for (int k = 0; k < M; ++k) {
+            for (int k = 0; k < MQ; ++k) {
                 const double ai = lo ? x[k] : px[k], aj = lo ? px[k] : x[k];
-                alpha += ai * ai;
-                beta += aj * aj;
-                gamma += ai * aj;
+                pa += ai * ai;
+                pb += aj * aj;
+                pg += ai * aj;
             }
+            const double alpha = quad_sum_f64(pa), beta = quad_sum_f64(pb), gamma = quad_sum_f64(pg);
             if (alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta))) {
                 changed = true;
                 const double zeta = (beta - alpha) / (2.0 * gamma);
-                double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                if (zeta < 0) t = -t;
-                const double c = 1.0 / sqrt(1.0 + t * t);
-                const double s = c * t;
+                const double u = fabs(zeta) + sqrt(1.0 + zeta * zeta);
+                const double wn = sqrt(u * u + 1.0);
+                const double c = u / wn;
+                const double s = (zeta < 0 ? -1.0 : 1.0) / wn;
 #pragma unroll
-                for (int k = 0; k < M; ++k) {
+                for (int k = 0; k < MQ; ++k) {
                     const double xi = lo ? x[k] : px[k], xj = lo ? px[k] : x[k];
                     x[k] = lo ? c * xi - s * xj : s * xi + c * xj;
                 }
 #pragma unroll
-                for (int k = 0; k < N; ++k) {
+                for (int k = 0; k < NQ; ++k) {
                     const double vi = lo ? v[k] : pv[k], vj = lo ? pv[k] : v[k];
                     v[k] = lo ? c * vi - s * vj : s * vi + c * vj;
                 }
             }
         }
-        if (__ballot(lane < N && changed) == 0) break;
+        if (__ballot(act && changed) == 0) break;
     }
-    if (lane < N) {
+    // column norms in the same quarter order, then the oracle's sort and normalisation
+    double pn = 0;
 #pragma unroll
-        for (int k = 0; k < M; ++k) A[k * N + col] = x[k];
+    for (int k = 0; k < MQ; ++k) pn += x[k] * x[k];
+    const double nn = quad_sum_f64(pn);
+    if (act) {
 #pragma unroll
-        for (int k = 0; k < N; ++k) V[k * N + col] = v[k];
-    }
-    wave_lds_sync();
-    for (int i = 0; i < N; ++i) {
-        double s = 0;
+        for (int k = 0; k < MQ; ++k) A[(q * MQ + k) * N + col] = x[k];
 #pragma unroll
-        for (int k = 0; k < M; ++k) s += A[k * N + i] * A[k * N + i];
-        if (lane == 0) w[i] = sqrt(s);
+        for (int k = 0; k < NQ; ++k) V[(q * NQ + k) * N + col] = v[k];
+        if (q == 0) w[col] = sqrt(nn);
     }
     wave_lds_sync();
     for (int i = 0; i < N - 1; ++i) {

@@ -97,12 +97,27 @@ static void svd_jacobi(double* A, int m, int n, double* w, double* V)
     }
 }
 
-/* Round-robin ("parallel ordering") one-sided Jacobi SVD for even n.  Each sweep runs n-1
- * rounds; round r pairs the columns by the circle method (column 0 fixed, the others
- * rotated by r), so a round's rotations touch disjoint column pairs and may be applied in any
- * order (or all at once, as the GPU does).  Same per-rotation arithmetic, stopping rule,
- * sort and normalisation as svd_jacobi; used for EPnP's 12x12 M^T M.  (OpenCV's JacobiSVD
- * uses the cyclic order; the decompositions agree to rounding -- OpenCV-level parity is
+/* Sum over k of f(k) for k = 0..m-1 (m a multiple of 4) in the order the GPU's quad of lanes
+ * forms it: four serial partial sums over the row quarters, then (p0 + p1) + (p2 + p3). */
+#define QUARTER_SUM(res, m, expr)                                              \
+    do {                                                                       \
+        double qs_[4] = {0, 0, 0, 0};                                          \
+        const int qm_ = (m) / 4;                                               \
+        for (int q_ = 0; q_ < 4; ++q_)                                         \
+            for (int k = q_ * qm_; k < (q_ + 1) * qm_; ++k) qs_[q_] += (expr); \
+        (res) = (qs_[0] + qs_[1]) + (qs_[2] + qs_[3]);                         \
+    } while (0)
+
+/* Round-robin ("parallel ordering") one-sided Jacobi SVD for even n and m a multiple of 4
+ * (EPnP's 12x12 M^T M).  Each sweep runs n-1 rounds; round r pairs the columns by the circle
+ * method (column 0 fixed, the others rotated by r), so a round's rotations touch disjoint
+ * column pairs and may be applied in any order (or all at once, as the GPU does).  The GPU
+ * gives every column four lanes (one row quarter each), so the column dot products are
+ * quarter-wise partial sums combined pairwise (QUARTER_SUM), and the rotation is formed as
+ * u = |zeta| + sqrt(1 + zeta^2), w = sqrt(u^2 + 1), c = u / w, s = sign(zeta) / w -- the same
+ * rotation as t = sign / u, c = 1 / sqrt(1 + t^2), s = c t, one dependent division shorter.
+ * Stopping rule, sort and normalisation as svd_jacobi.  (OpenCV's JacobiSVD uses the cyclic
+ * order and its own summation; the decompositions agree to rounding -- OpenCV-level parity is
  * unpinned anyway, and the GPU follows this order exactly.) */
 static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
 {
@@ -115,21 +130,18 @@ static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
                 const int a = q == 0 ? 0 : ((q - 1 + r) % (n - 1)) + 1;
                 const int b = ((n - 2 - q + r) % (n - 1)) + 1;
                 const int i = a < b ? a : b, j = a < b ? b : a;
-                double alpha = 0, beta = 0, gamma = 0;
-                for (int k = 0; k < m; ++k) {
-                    double ai = A[k * n + i], aj = A[k * n + j];
-                    alpha += ai * ai;
-                    beta += aj * aj;
-                    gamma += ai * aj;
-                }
+                double alpha, beta, gamma;
+                QUARTER_SUM(alpha, m, A[k * n + i] * A[k * n + i]);
+                QUARTER_SUM(beta, m, A[k * n + j] * A[k * n + j]);
+                QUARTER_SUM(gamma, m, A[k * n + i] * A[k * n + j]);
                 if (alpha == 0.0 || beta == 0.0) continue;
                 if (fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
                 changed = 1;
-                double zeta = (beta - alpha) / (2.0 * gamma);
-                double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                if (zeta < 0) t = -t;
-                double c = 1.0 / sqrt(1.0 + t * t);
-                double s = c * t;
+                const double zeta = (beta - alpha) / (2.0 * gamma);
+                const double u = fabs(zeta) + sqrt(1.0 + zeta * zeta);
+                const double wn = sqrt(u * u + 1.0);
+                const double c = u / wn;
+                const double s = (zeta < 0 ? -1.0 : 1.0) / wn;
                 for (int k = 0; k < m; ++k) {
                     double ai = A[k * n + i], aj = A[k * n + j];
                     A[k * n + i] = c * ai - s * aj;
@@ -145,8 +157,8 @@ static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
         if (!changed) break;
     }
     for (int i = 0; i < n; ++i) {
-        double s = 0;
-        for (int k = 0; k < m; ++k) s += A[k * n + i] * A[k * n + i];
+        double s;
+        QUARTER_SUM(s, m, A[k * n + i] * A[k * n + i]);
         w[i] = sqrt(s);
     }
     for (int i = 0; i < n - 1; ++i) {

@@ -3,7 +3,9 @@ sequence (4541 frames), against the reference class's own runs (tests/golden/
 make_long_golden.py: /root/reference/VisualOdometryPipeLine.py on the oracle primitives):
 
 * one chain over all 4541 frames (main.py:112-124, :166-175): every pose and num_pts entry
-  bit-identical, so the ATE against the reference trajectory is 0;
+  bit-identical, so the ATE against the reference trajectory is 0, and where the reference run
+  stops with an exception the chain stops at the same frame with the matching status (the
+  current fixture: "Not enough keypoints for PnP" at frame 4535, 4533 poses);
 * the sequence cut into 16 and into 8 shards (C4's layout) on the same boundaries as the
   reference runs: every shard's trajectory bit-identical to its reference run, no failed
   shard and no coverage break in the stitched trajectory.
@@ -45,8 +47,12 @@ def test_full_sequence_matches_reference():
     from monocular_visual_odometry_va4mr_amd import options as Op
     from monocular_visual_odometry_va4mr_amd.ate import ate
     from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd import _lib as L
     g = _load("kitti_seq00.npz")
-    assert str(g["error"]) == "", "the reference run itself must track every frame"
+    err = str(g["error"])
+    # the reference run either tracks every frame or stops with one of its ValueErrors, which
+    # the chain must reproduce as its status (_lib.STATUS_NAMES)
+    want = 0 if err == "" else next(k for k, m in L.STATUS_NAMES.items() if k != 0 and m in err)
     dev = torch.device("cuda")
     r, frames = _render_all(g, dev)
     n = frames.shape[0]
@@ -60,14 +66,19 @@ def test_full_sequence_matches_reference():
     for i in range(b1 + 1, n):
         eng.step(frames[i:i + 1])
     torch.cuda.synchronize()
-    assert int(eng.t["status"][0]) == 0
+    assert int(eng.t["status"][0]) == want, (int(eng.t["status"][0]), err)
     nF = int(eng.t["nF"][0])
     t = eng.t["pose_t"][0, 1:nF].cpu().numpy()
     npts = eng.t["num_pts"][0, 1:nF].cpu().numpy()
     assert t.shape == g["t"].shape
     assert np.array_equal(t, g["t"]), f"first differing pose at record {np.nonzero((t != g['t']).any(1))[0][:1]}"
     assert np.array_equal(npts, g["num_pts"])
-    assert int(eng.t["nL"][0]) == int(g["N"][-1]) and int(eng.t["nC"][0]) == int(g["P"][-1])
+    if want == 0:
+        assert int(eng.t["nL"][0]) == int(g["N"][-1]) and int(eng.t["nC"][0]) == int(g["P"][-1])
+    elif want == L.ST_NOT_ENOUGH_KP:
+        # VisualOdometryPipeLine.py:342,357-358: the step that raised tracked fewer than 8
+        # landmarks; the fixture records counts only for the frames that completed
+        assert int(eng.t["nL"][0]) < 8 <= int(g["N"][-1])
     rmse, rel = ate(t, g["t"])
     assert rel == 0.0 or rel < 1e-12
 
