@@ -329,6 +329,21 @@ class Engine:
         self.replay_step()
 
     # ------------------------------------------------------------------ bootstrap
+    def reserve_bootstrap(self, sift_batch_bytes: int | None = None):
+        """Allocate the SIFT scale-space workspace bootstrap() uses (SIFT_create at
+        VisualOdometryPipeLine.py:35 is likewise done once, in the constructor); bootstrap()
+        calls it itself when nothing is reserved.  Returns (Sift, chains per chunk)."""
+        from .features import Sift
+        budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 24 << 30))
+        per_img = Sift.bytes_per_image(self.W, self.H)
+        m = max(1, min(self.B, budget // (2 * per_img)))     # chains per chunk
+        nfeat = int(self.options.get("sift_nfeatures", 0))    # C5: SIFT_create(8192)
+        if getattr(self, "_sift", None) is None or self._sift.batch < 2 * m or self._sift.nfeatures != nfeat:
+            self._sift = None
+            torch.cuda.empty_cache()
+            self._sift = Sift(self.W, self.H, self.device, batch=2 * m, nfeatures=nfeat)
+        return self._sift, m
+
     def bootstrap(self, img0, img1, sift_batch_bytes: int | None = None):
         """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:
         SIFT on both frames, BF 2-NN + ratio test, 5-point E-RANSAC, inlier split,
@@ -337,25 +352,17 @@ class Engine:
         preset's 8192) is SIFT_create(nfeatures).
 
         Batched across chains: the chains are taken in chunks whose SIFT scale spaces fit
-        ``sift_batch_bytes`` (default 12 GB, env VO_SIFT_BATCH_BYTES); per chunk one
+        ``sift_batch_bytes`` (default 24 GB, env VO_SIFT_BATCH_BYTES); per chunk one
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync until
         the SIFT capacity check, which comes before any chain state is written."""
-        from .features import Sift, bf_knn2_batch
+        from .features import bf_knn2_batch
         img0 = self._frames(img0)
         img1 = self._frames(img1)
         d = self.dims
         dev = self.device
         B = self.B
-        budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 12 << 30))
-        per_img = Sift.bytes_per_image(self.W, self.H)
-        m = max(1, min(B, budget // (2 * per_img)))          # chains per chunk
-        nfeat = int(self.options.get("sift_nfeatures", 0))    # C5: SIFT_create(8192)
-        if getattr(self, "_sift", None) is None or self._sift.batch < 2 * m or self._sift.nfeatures != nfeat:
-            self._sift = None
-            torch.cuda.empty_cache()
-            self._sift = Sift(self.W, self.H, dev, batch=2 * m, nfeatures=nfeat)
-        sift = self._sift
+        sift, m = self.reserve_bootstrap(sift_batch_bytes)
         kcap = sift.kp_cap
         cap = min(d.ncap, d.pcap, kcap)
         pts0 = torch.zeros((B, cap, 2), dtype=torch.float32, device=dev)
