@@ -15,7 +15,7 @@ golden of the same sequence -- the trajectory the GPU reproduces bit for bit -- 
 * LK sums in float: the monocular chain is chaotic -- a 0.05 px change in one tracked point
   flips a RANSAC inlier -- and ends 5.1 % (C2, over the 4533 poses both runs have; the float
   run tracks on to frame 4540) / 5.0 % (Parking, 94) / 2e-6 (Malaga 1024, 34) of the path
-  away, while both trajectories drift 21-24 % from ground truth.
+  away (profiles/r3_opencv_fp32_trajectory.json).
   A 1 % bound against a real OpenCV run therefore needs OpenCV's own float summation order
   (its SSE lane grouping), which no OpenCV in this image can pin: recorded as unpinned
   (DESIGN.md §3)."""

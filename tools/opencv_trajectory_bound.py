@@ -18,6 +18,8 @@ fixture (tests/golden/opencv_fp32_trajectories.npz).  tests/test_opencv_deviatio
 the ATE (Umeyama Sim(3) RMSE relative to the path length) of each against the
 integer-mode golden -- the trajectory the GPU reproduces bit for bit -- next to north_star's
 1 % tolerance.  Usage: python tools/opencv_trajectory_bound.py [--procs 6] [--cases ...]
+[--summary-only]; the ATE table (against the integer golden) goes to
+profiles/r3_opencv_fp32_trajectory.json.
 """
 from __future__ import annotations
 
@@ -90,11 +92,40 @@ def _run(args):
     return case, mode, np.stack(ts), np.array(npts, np.int32), err
 
 
+def summary(path=os.path.join(REPO, "profiles", "r3_opencv_fp32_trajectory.json")):
+    """ATE of every fp32-mode trajectory against the integer golden (over the poses both runs
+    have)."""
+    import json
+    from monocular_visual_odometry_va4mr_amd.ate import ate
+    fx = np.load(OUT, allow_pickle=False)
+    rep = {"tool": "tools/opencv_trajectory_bound.py", "fixture": "tests/golden/opencv_fp32_trajectories.npz",
+           "ate": "Umeyama Sim(3) RMSE / path length of the integer-mode trajectory, over the poses both runs have",
+           "north_star_tolerance": 0.01, "cases": {}}
+    for case in CASES:
+        g = np.load(os.path.join(REPO, "tests", "golden", f"{case}.npz"), allow_pickle=False)
+        ref = g["t"].reshape(len(g["t"]), 3)
+        c = {"frames": int(len(ref)), "error": str(g["error"])}
+        for m, name in ((1, "gftt_fp32"), (2, "lk_fp32_sums"), (3, "both")):
+            t = fx[f"{case}_m{m}_t"]
+            k = min(len(t), len(ref))
+            c[name] = {"frames": int(len(t)), "error": str(fx[f"{case}_m{m}_error"]),
+                       "identical_to_integer_golden": bool(len(t) == len(ref) and np.array_equal(t, ref)),
+                       "ate_vs_integer": float(ate(t[:k], ref[:k])[1])}
+        rep["cases"][case] = c
+    with open(path, "w") as f:
+        json.dump(rep, f, indent=1)
+    print("wrote", path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=6)
     ap.add_argument("--cases", nargs="*", default=list(CASES))
+    ap.add_argument("--summary-only", action="store_true")
     a = ap.parse_args()
+    if a.summary_only:
+        summary()
+        return
     for c in a.cases:           # render the long sequence once, before the workers fork
         if c == "kitti_seq00":
             _frames(c)
@@ -108,6 +139,7 @@ def main():
             out[f"{case}_m{mode}_error"] = np.asarray(err)
             np.savez_compressed(OUT, **out)             # keep what is done so far
     print("wrote", OUT)
+    summary()
 
 
 if __name__ == "__main__":
