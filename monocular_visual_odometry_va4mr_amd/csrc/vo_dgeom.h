@@ -478,6 +478,68 @@ VO_DEV int real_roots(const double* c_in, int deg, double* roots)
     return nr;
 }
 
+// real_roots<D> computed by the four lanes of a quad together (sub = lane & 3; every lane of
+// the quad calls it with the same coefficients): lane k brackets interval k + 1 of the serial
+// walk -- the same peval / bracket_root calls on the same values -- and the roots are gathered
+// in interval order, so the result is bit-identical to real_roots<D> while the quad's serial
+// chain is one bracket per degree instead of up to D.
+template <int D>
+VO_DEV int real_roots_q(const double* c_in, int deg, double* roots, int sub);
+
+template <>
+VO_DEV int real_roots_q<2>(const double* c_in, int deg, double* roots, int sub)
+{
+    (void)sub;
+    return real_roots<2>(c_in, deg, roots);
+}
+
+template <int D>
+VO_DEV int real_roots_q(const double* c_in, int deg, double* roots, int sub)
+{
+    while (deg > 0 && c_in[deg] == 0.0) --deg;
+    if (deg <= 0) return 0;
+    if (deg < D) return real_roots_q<D - 1>(c_in, deg, roots, sub);
+    double c[D + 1];
+    for (int i = 0; i <= D; ++i) c[i] = c_in[i] / c_in[D];
+    double dc[D];
+    for (int i = 1; i <= D; ++i) dc[i - 1] = c[i] * i;
+    double crit[D];
+    int nc = real_roots_q<D - 1>(dc, D - 1, crit, sub);
+    double bound = 0;
+    for (int i = 0; i < D; ++i) if (fabs(c[i]) > bound) bound = fabs(c[i]);
+    bound += 1.0;
+    double pts[D + 2];
+    int np = 0;
+    pts[np++] = -bound;
+    for (int i = 0; i < nc; ++i) if (crit[i] > -bound && crit[i] < bound) pts[np++] = crit[i];
+    pts[np++] = bound;
+    // interval k = sub + 1 of the serial walk (fprev there is peval(pts[k - 1]))
+    double rk = 0.0;
+    int has = 0;
+    {
+        const int k = sub + 1;
+        if (k < np) {
+            double lo = pts[0], hi = pts[1];
+#pragma unroll
+            for (int i = 1; i < D + 1; ++i)
+                if (i == k) { lo = pts[i - 1]; hi = pts[i]; }         // constant indices
+            const double fprev = peval(c, D, lo);
+            const double f = peval(c, D, hi);
+            if (f == 0.0) { rk = hi; has = 1; }
+            else if (fprev != 0.0 && ((f < 0) != (fprev < 0))) { rk = bracket_root(c, dc, D, lo, hi, fprev); has = 1; }
+        }
+    }
+    const int base = lane_id() & ~3;
+    int nr = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const int hj = __shfl(has, base | j, 64);
+        const double rj = __shfl(rk, base | j, 64);
+        if (j + 1 < np && hj) roots[nr++] = rj;
+    }
+    return nr;
+}
+
 // ------------------------------------------------------------------ P3P
 struct CamK {
     double fx, fy, cx, cy, ifx, ify, cx_fx, cy_fx;
@@ -577,7 +639,8 @@ VO_DEV void align_horn(const double M[3][3], const double P[3][3], double* R, do
     for (int i = 0; i < 3; ++i) T[i] = cm[i] - (R[i * 3] * cp[0] + R[i * 3 + 1] * cp[1] + R[i * 3 + 2] * cp[2]);
 }
 
-VO_DEV int p3p_lengths(double L[4][3], const double d[3], const double cs[3])
+// sub < 0: serial root finder; sub = lane & 3: the quad-cooperative one (identical roots)
+VO_DEV int p3p_lengths(double L[4][3], const double d[3], const double cs[3], int sub = -1)
 {
     double p = cs[0] * 2, q = cs[1] * 2, r = cs[2] * 2;
     double inv_d22 = 1. / (d[2] * d[2]);
@@ -598,7 +661,7 @@ VO_DEV int p3p_lengths(double L[4][3], const double d[3], const double cs[3])
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) if (i + j < 5) c[i + j] -= b * r * Nn[i] * xLp[j];
     for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) c[i + j] -= b * Qq[i] * LL[j];
     double xs[4];
-    int nr = real_roots<4>(c, 4, xs);
+    int nr = sub < 0 ? real_roots<4>(c, 4, xs) : real_roots_q<4>(c, 4, xs, sub);
     int ns = 0;
     for (int i = 0; i < nr; ++i) {
         double x = xs[i];
@@ -655,7 +718,7 @@ VO_DEV int p3p_solution(const CamK& k, const double* obj, const double* img_px, 
     cs[1] = mu[0] * mu[2] + mv[0] * mv[2] + mk[0] * mk[2];
     cs[2] = mu[0] * mu[1] + mv[0] * mv[1] + mk[0] * mk[1];
     double L[4][3];
-    const int n = p3p_lengths(L, dist, cs);
+    const int n = p3p_lengths(L, dist, cs, sol);      // the quad's four lanes find the roots together
     if (sol >= n) return 0;
     double l0 = 0, l1 = 0, l2 = 0;          // L[sol] selected with constant indices
 #pragma unroll

@@ -60,18 +60,19 @@ __global__ void k_t_p3p_parts(const double* K, const double* pws, const double* 
             for (int q = 0; q < 2; ++q) im[2 * j + q] = us[2 * id + q];
         }
     };
-    // lane 0 alone: lengths (quartic) then one align
-    if (lane == 0) {
+    // lanes 0..3 (one hypothesis' quad): serial lengths (quartic) on each, then one solution
+    // per lane (the quad-cooperative root finder needs all four lanes)
+    if (lane < 4) {
         load(0);
         double dist[3] = {1.0, 1.2, 0.9}, cs[3] = {0.99, 0.98, 0.985}, L[4][3];
         long long a0 = wall_clock64();
         int ns = vg::p3p_lengths(L, dist, cs);
         long long a1 = wall_clock64();
-        int ok = vg::p3p_solution(k, o, im, 0, R, T, &e);
+        int ok = vg::p3p_solution(k, o, im, lane, R, T, &e);
         long long a2 = wall_clock64();
         int ok2 = vg::p3p_solve4(k, o, im, R, T);
         long long a3 = wall_clock64();
-        t[0] = a1 - a0; t[1] = a2 - a1; t[2] = a3 - a2; t[3] = ns + 10 * ok + 100 * ok2;
+        if (lane == 0) { t[0] = a1 - a0; t[1] = a2 - a1; t[2] = a3 - a2; t[3] = ns + 10 * ok + 100 * ok2; }
     }
     __syncthreads();
     // 64 lanes, one hypothesis each, serial solutions (old layout)
