@@ -34,7 +34,9 @@ def main():
     m = counters([sq1, sq2])["k_lk_w"]
     b = json.load(open(bj))
     pts = float(b["points_last_step"])
-    rec = {"kernel": "k_lk_w", "tag": tag, "chains": b["config"]["chains_per_gpu"], "points_per_launch": pts,
+    # one k_lk_w launch tracks one stream group's chains (points_last_step counts group 0's)
+    per_launch = b["config"]["chains_per_gpu"] // max(1, int(b["config"].get("streams_per_gpu", 1)))
+    rec = {"kernel": "k_lk_w", "tag": tag, "chains_per_launch": per_launch, "points_per_launch": pts,
            "valu_insts_per_launch": m["SQ_INSTS_VALU"], "salu_insts_per_launch": m.get("SQ_INSTS_SALU"),
            "lds_insts_per_launch": m.get("SQ_INSTS_LDS"), "waves_per_launch": m.get("SQ_WAVES"),
            "valu_per_point": m["SQ_INSTS_VALU"] / pts,
