@@ -65,6 +65,39 @@ VO_DEV void wave_sum2_dpp(int& x, int& y)
     y = __builtin_amdgcn_readlane(y, 63);
 }
 
+// Two wave sums in one DPP chain: v_permlane32_swap trades the upper half of x for the lower
+// half of y, so one add leaves x's half-sums in lanes 0..31 and y's in 32..63; five row-level
+// steps finish both (totals in lanes 31 and 63).  Exact for int32 partials whose sums fit.
+VO_DEV void wave_sum2_swap(int& x, int& y)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    int v = (int)r[0] + (int)r[1];
+    v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x = __builtin_amdgcn_readlane(v, 31);
+    y = __builtin_amdgcn_readlane(v, 63);
+}
+
+// Three wave sums: x and y share one chain through the half swap (as wave_sum2_swap), z runs
+// its own six steps interleaved with it.
+VO_DEV void wave_sum3_swap(int& x, int& y, int& z)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    int v = (int)r[0] + (int)r[1];
+#define VO_DPP2(ctl, rm) \
+    v += __builtin_amdgcn_update_dpp(0, v, ctl, rm, 0xF, false); \
+    z += __builtin_amdgcn_update_dpp(0, z, ctl, rm, 0xF, false);
+    VO_DPP2(0xB1, 0xF) VO_DPP2(0x4E, 0xF) VO_DPP2(0x124, 0xF) VO_DPP2(0x128, 0xF) VO_DPP2(0x142, 0xA)
+#undef VO_DPP2
+    z += __builtin_amdgcn_update_dpp(0, z, 0x143, 0xC, 0xF, false);
+    x = __builtin_amdgcn_readlane(v, 31);
+    y = __builtin_amdgcn_readlane(v, 63);
+    z = __builtin_amdgcn_readlane(z, 63);
+}
+
 VO_DEV void wave_sum3_dpp(int& x, int& y, int& z)
 {
 #define VO_DPP3(ctl, rm) \

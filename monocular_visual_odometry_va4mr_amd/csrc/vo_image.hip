@@ -348,12 +348,14 @@ VO_DEV void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// a wave-uniform VALU result into an SGPR: the readfirstlane of an opaque VALU value cannot
-// be moved ahead of the conversion that produced it, so the arithmetic that consumes it (the
-// weight packing) runs on the scalar unit instead of the VALU
+// a wave-uniform VALU result into an SGPR, where the arithmetic that consumes it (the weight
+// packing) runs on the scalar unit instead of the VALU
 VO_DEV int to_sgpr(int v)
 {
-    return __builtin_amdgcn_readfirstlane(v + opaque0());
+    // an empty asm makes the VGPR value opaque, so the readfirstlane cannot be folded into the
+    // conversion that produced it (an inline-asm readfirstlane instead broke LK on gfx950)
+    asm volatile("" : "+v"(v));
+    return __builtin_amdgcn_readfirstlane(v);
 }
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 VO_DEV v2i16 as_v2i16(uint32_t u) { return __builtin_bit_cast(v2i16, u); }
@@ -648,6 +650,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     if (n1 <= P.seg1_min) n1 = 0;
     const int ntot = n0 + n1;
     const float hx = (WW - 1) * 0.5f, hy = (WH - 1) * 0.5f;
+    // held in registers: read from the kernel arguments inside the iteration loop it costs a
+    // scalar load and its wait per iteration
+    double eps2;
+    asm volatile("" : "=s"(eps2) : "0"(P.eps2));
     // window pixels of a lane: column lane % 16, rows 4 j + s with s = (lane / 32) + 2 (lane / 16
     // % 2), so that a 32-lane half reads rows s and s + 2 (row offsets 0 and 2 * QS = 48 dwords,
     // 16 banks apart: conflict-free) and pixel j sits at the constant offset toff + 4 j QS
@@ -859,7 +865,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const float FLT_SCALE = 1.f / (1 << 20);
                 float A11, A12, A22;
                 if (!twide) {
-                    wave_sum3_dpp(a11, a12, a22);
+                    wave_sum3_swap(a11, a22, a12);
                     A11 = (float)a11 * FLT_SCALE; A12 = (float)a12 * FLT_SCALE; A22 = (float)a22 * FLT_SCALE;
                 } else {
                     A11 = (float)wave_sum_split(a11) * FLT_SCALE; A12 = (float)wave_sum_split(a12) * FLT_SCALE;
@@ -877,26 +883,35 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 LKPROF_T(ta1);
                 LKPROF_ADD(5, ta1 - ti1);
                 for (int it = 0; it < P.max_count; ++it) {
-                    const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+                    // floor(n) as a float is exact, so n - floor(n) == n - (float)(int)floor(n)
+                    const float fnx = floorf(nx), fny = floorf(ny);
+                    const int inx = (int)fnx, iny = (int)fny;
                     if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
                         if (level == 0) status = 0;
                         break;
                     }
-                    if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) {
+                    if (!staged || (unsigned)(inx - tx0) > 2u * LK_M || (unsigned)(iny - ty0) > 2u * LK_M) {
                         stage_j(inx, iny);
                         staged = true;
                     }
-                    a = nx - inx;
-                    bb = ny - iny;
-                    // wave-uniform weights: into scalar registers, packed by the scalar unit
-                    const int w00 = to_sgpr(__float2int_rn((1.f - a) * (1.f - bb) * (float)(1 << 14)));
-                    const int w01 = to_sgpr(__float2int_rn(a * (1.f - bb) * (float)(1 << 14)));
-                    const int w10 = to_sgpr(__float2int_rn((1.f - a) * bb * (float)(1 << 14)));
-                    const int w11 = (1 << 14) - w00 - w01 - w10;
+                    a = nx - fnx;
+                    bb = ny - fny;
+                    // wave-uniform weights: into scalar registers, packed by the scalar unit.
+                    // cvRound(w) for w in [0, 2^14] is the low bits of the float w + 1.5 * 2^23
+                    // (the add rounds half to even at unit spacing, as rint does), so one VALU add
+                    // replaces round + convert; the bit fields the packing takes are those of w.
+                    // (x * y) * 2^14 == (x * 2^14) * y exactly (power-of-two scaling, normal
+                    // range), so the three products share two scaled factors.
+                    const float LK_RND = 12582912.f;
+                    const float xa = (1.f - a) * (float)(1 << 14), ya = 1.f - bb;
+                    const uint32_t u00 = (uint32_t)to_sgpr(__float_as_int(xa * ya + LK_RND));
+                    const uint32_t u01 = (uint32_t)to_sgpr(__float_as_int((a * (float)(1 << 14)) * ya + LK_RND));
+                    const uint32_t u10 = (uint32_t)to_sgpr(__float_as_int(xa * bb + LK_RND));
+                    const int w11 = (int)((1u << 14) + 3u * 0x4B400000u - u00 - u01 - u10);
                     // iw11 can be -1: dot with w11 + 1 and subtract the tap once
                     const int neg = w11 < 0;
-                    const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
-                    const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
+                    const uint32_t wlo = pack_w((int)u00, (int)u01, (int)u10, w11 + neg, 0, 127);
+                    const uint32_t whi = pack_w((int)u00, (int)u01, (int)u10, w11 + neg, 7, 255);
                     const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int b1 = 0, b2 = 0;
                     // all four quads read before the (wave-uniform) branch: one LDS round trip
@@ -922,7 +937,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                                                (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
                     // int32 -> float and int64 -> float round the same integer identically
                     float fb1, fb2;
-                    if (!wide) { wave_sum2_dpp(b1, b2); fb1 = (float)b1 * FLT_SCALE; fb2 = (float)b2 * FLT_SCALE; }
+                    if (!wide) {
+                        wave_sum2_swap(b1, b2);
+                        fb1 = (float)b1 * FLT_SCALE; fb2 = (float)b2 * FLT_SCALE;
+                    }
                     else { fb1 = (float)wave_sum_split(b1) * FLT_SCALE; fb2 = (float)wave_sum_split(b2) * FLT_SCALE; }
                     const float ddx = (A12 * fb2 - A22 * fb1) * D;
                     const float ddy = (A12 * fb1 - A11 * fb2) * D;
@@ -930,7 +948,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     ny += ddy;
                     ox = nx + hx;
                     oy = ny + hy;
-                    if ((double)ddx * ddx + (double)ddy * ddy <= P.eps2) break;
+                    // squares of floats are exact in double, so one fma rounds the same sum
+                    const double dy2 = (double)ddy * ddy;
+                    if (__builtin_fma((double)ddx, (double)ddx, dy2) <= eps2) break;
                     if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
                         ox -= ddx * 0.5f;
                         oy -= ddy * 0.5f;
