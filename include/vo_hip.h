@@ -169,6 +169,11 @@ int vo_gftt_eigmap(const vo_dims* d, const vo_opts* o, const vo_state* s, int cu
  * (:371-373).  Call after vo_gftt. */
 int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
 
+/* Chain 0's (status, inlier count) written by one kernel into dst[0..1], which may be pinned host
+ * memory: what the drop-in class checks after every frame to raise the reference's ValueErrors
+ * (:352, :358) and to append len(inlier_pts_current) (:360-364), without a gather + copy. */
+int vo_status_word(const vo_state* s, int32_t* dst, vo_stream_t stream);
+
 /* ---- single-call primitives for the cv2 surface (B1) --------------------------- */
 
 /* cv2.calcOpticalFlowPyrLK (:281,287): points [B][n] with per-chain counts, using the

@@ -137,6 +137,7 @@ def _declare(L):
         "vo_gftt": ([D, O, S, C.c_int, P], C.c_int),
         "vo_gftt_eigmap": ([D, O, S, C.c_int, P], C.c_int),
         "vo_add_corners_finish": ([D, O, S, P], C.c_int),
+        "vo_status_word": ([S, P, P], C.c_int),
         "vo_lk_points": ([D, O, S, C.c_int, P, P, i32, P, P, P, P], C.c_int),
         "vo_pnp_ransac": ([O, C.c_int, P, P, P, i32, P, P, P, P, P, P, i64, P], C.c_int),
         "vo_triangulate_points": ([C.c_int, P, P, P, P, P, P], C.c_int),

@@ -14,9 +14,19 @@ using namespace vg;
 
 #ifdef VO_PNP_PROF
 __device__ long long g_pnpprof[32];
+}  // namespace
+// diagnostics build only (libvo_hip_pnpprof.so, tools/pnp_prof.py): block 0's phase timestamps
+// of the last PnP launch (100 MHz wall clock)
+extern "C" int vo_pnp_prof_read(long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pnpprof), sizeof(long long) * 32) == hipSuccess ? 0 : -2;
+}
+namespace {
 #define PNPPROF(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pnpprof[i] = wall_clock64(); } while (0)
+#define PNPVAL(i, v) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pnpprof[i] = (v); } while (0)
 #else
 #define PNPPROF(i) do { } while (0)
+#define PNPVAL(i, v) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------ EPnP (block)
@@ -498,8 +508,11 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
         PNPPROF(6);
         {
             // four lanes per hypothesis, one P3P solution each (p3p_solution); the lanes then
-            // apply p3p_solve4's rule (first solution with a strictly smaller 4th-point error)
-            const int h = tid >> 2, sol = tid & 3, lane = lane_id();
+            // apply p3p_solve4's rule (first solution with a strictly smaller 4th-point error).
+            // The hypotheses are spread over all waves (CH / waves each): a wave's P3P time is
+            // that of its slowest root bracketing / eigen-sweep count, so fewer per wave finish sooner.
+            const int lane = lane_id(), hpw = CH / (blockDim.x >> 6), hq = lane >> 2, sol = lane & 3;
+            const int h = hq < hpw ? wave_id() * hpw + hq : CH;
             double R[9], t[3], e = 0.0;
             int ok = 0;
             if (h < CH && it0 + h < niters0) {
@@ -530,39 +543,51 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
         __syncthreads();
         PNPPROF(2);
         {
-            const int w = wave_id(), lane = lane_id();
-            const int hpw = CH / (blockDim.x >> 6);
-            for (int h = w * hpw; h < (w + 1) * hpw; ++h) {
-                if (!valid[h]) { if (lane == 0) cnt[h] = 0; continue; }
-                const double* R = mdl[h];
-                const double* t = mdl[h] + 9;
-                int c = 0;
-                for (int i = lane; i < n; i += 64)
-                    c += pnp_err(R, t, k, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= A.thr;
-                c = wave_sum_i32(c);
-                if (lane == 0) cnt[h] = c;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int niters = sh[1], best = sh[2];
-            for (int h = 0; h < CH; ++h) {
-                if (it0 + h >= niters) break;
-                if (!valid[h]) continue;
-                const int good = cnt[h];
-                if (good > (best > 3 ? best : 3)) {
-                    best = good;
-                    for (int q = 0; q < 12; ++q) bestm[q] = mdl[h][q];
-                    niters = ransac_update_niters(A.conf, (double)(n - good) / n, 4, niters);
+            // scoring in the order the sequential rule below visits the hypotheses, one per wave
+            // at a time: a hypothesis at or past the running adaptive iteration count is never
+            // looked at, so the batches stop once it is reached (same result as scoring all CH)
+            const int w = wave_id(), lane = lane_id(), nw = blockDim.x >> 6;
+            for (int h0 = 0; h0 < CH; h0 += nw) {
+                if (it0 + h0 >= sh[1]) break;                         // block-uniform
+                const int h = h0 + w;
+                if (h < CH) {
+                    int c = 0;
+                    if (valid[h]) {
+                        const double* R = mdl[h];
+                        const double* t = mdl[h] + 9;
+                        for (int i = lane; i < n; i += 64)
+                            c += pnp_err(R, t, k, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= A.thr;
+                        c = wave_sum_i32(c);
+                    }
+                    if (lane == 0) cnt[h] = c;
                 }
+                __syncthreads();
+                if (tid == 0) {
+                    int niters = sh[1], best = sh[2];
+                    const int h1 = h0 + nw < CH ? h0 + nw : CH;
+                    for (int hh = h0; hh < h1; ++hh) {
+                        if (it0 + hh >= niters) break;
+                        if (!valid[hh]) continue;
+                        const int good = cnt[hh];
+                        if (good > (best > 3 ? best : 3)) {
+                            best = good;
+                            for (int q = 0; q < 12; ++q) bestm[q] = mdl[hh][q];
+                            niters = ransac_update_niters(A.conf, (double)(n - good) / n, 4, niters);
+                        }
+                    }
+                    sh[1] = niters;
+                    sh[2] = best;
+                }
+                __syncthreads();
             }
-            sh[0] = it0 + CH;
-            sh[1] = niters;
-            sh[2] = best;
         }
+        if (tid == 0) sh[0] = it0 + CH;
         __syncthreads();
     }
     PNPPROF(3);
+    PNPVAL(20, sh[0]);
+    PNPVAL(21, sh[1]);
+    PNPVAL(22, sh[2]);
     if (sh[2] <= 0) {
         if (tid == 0) { A.success[b] = 0; A.n_inl[b] = 0; }
         for (int i = tid; i < n; i += blockDim.x) mask[i] = 0;
@@ -630,9 +655,10 @@ VO_DEV void pnp_apply_block(const vo_dims& d, const vo_state& s, const double* r
         const bool in = valid && mask[i];
         float x0 = 0, x1 = 0, x2 = 0, k0 = 0, k1 = 0;
         if (valid) { x0 = X[3 * i]; x1 = X[3 * i + 1]; x2 = X[3 * i + 2]; k0 = kp[2 * i]; k1 = kp[2 * i + 1]; }
-        int tin, tout;
-        const int pin = nin + block_scan_flag(in, lds, &tin);
-        const int pout = nout + block_scan_flag(valid && !in, lds, &tout);
+        int tin;
+        const int pre = block_scan_flag(in, lds, &tin);                 // every thread before tid is valid
+        const int pin = nin + pre, pout = nout + (tid - pre);
+        const int tout = (n - base < (int)blockDim.x ? n - base : (int)blockDim.x) - tin;
         if (in) {
             X[3 * pin] = x0; X[3 * pin + 1] = x1; X[3 * pin + 2] = x2;
             kp[2 * pin] = k0; kp[2 * pin + 1] = k1;
@@ -753,7 +779,7 @@ VO_DEV void triangulate_block(const TriArgs& A)
 {
     __shared__ int lds[16];
     __shared__ double Rc[9], tc[3], Rcwc[9], tcwc[3], Pc[12];
-    __shared__ int sh_fail;
+    __shared__ int sh_fail, sh_m;
     const int b = blockIdx.x, tid = threadIdx.x;
     const vo_dims& d = A.d;
     const vo_state& s = A.s;
@@ -765,6 +791,7 @@ VO_DEV void triangulate_block(const TriArgs& A)
     const double* poset = s.pose_t + (int64_t)b * d.fcap * 3;
     if (tid == 0) {
         sh_fail = 0;
+        sh_m = 0;
         // current pose (R_CW, t_CW) is slot nF; (R_WC, t_WC) = (R^T, -R^T t)
         for (int i = 0; i < 9; ++i) Rc[i] = poseR[(int64_t)nF * 9 + i];
         for (int i = 0; i < 3; ++i) tc[i] = poset[(int64_t)nF * 3 + i];
@@ -777,76 +804,103 @@ VO_DEV void triangulate_block(const TriArgs& A)
     int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
     float* X = s.lm_X + (int64_t)b * d.ncap * 3;
     float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    // Three passes over the candidates (results identical to one pass, the reference's loop
+    // :171-206): (1) the frame gate and check_baseline, listing the candidates that reach
+    // cv2.triangulatePoints; (2) the triangulations, one listed candidate per thread -- the 4x4
+    // Jacobi SVD is a long serial FP64 chain, so a chunk of 256 candidates with a few of them
+    // triangulating cost as much as a chunk of 256 triangulations; (3) the ordered append /
+    // compaction.  Scratch: the list and flags in iwork, the points in work (PnP is done with it).
+    const int kmax = d.ncap > d.pcap ? d.ncap : d.pcap;
+    int32_t* tlist = s.iwork + (int64_t)b * d.iwork_stride;          // [m] candidate indices
+    int32_t* tacc = tlist + kmax;                                      // [nC] 1 = becomes a landmark
+    float* tX = (float*)(s.work + (int64_t)b * d.work_stride);          // [nC][3] its point
+    for (int i = tid; i < nC; i += blockDim.x) {
+        const float k0 = ck[2 * i], k1 = ck[2 * i + 1], f0 = cf[2 * i], f1 = cf[2 * i + 1];
+        const int tau = ct[i];
+        bool tri = false;
+        if (!(nF > 1 && nF - tau <= A.min_frames)) {                    // else retained, :175-178
+            const double* Rp = poseR + (int64_t)tau * 9;
+            // check_baseline :117-147: v_cur = K^-1 [u;1], v_past = ((R_cur^T R_past)^T K^-1) [u_f;1]
+            double vc[3], vp[3], rel[9], Mr[9];
+            const double uc[3] = {(double)k0, (double)k1, 1.0};
+            for (int r = 0; r < 3; ++r) vc[r] = dot_c102(A.Kinv + r * 3, uc);      // K_inv (C-order) @ v
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    rel[c * 3 + r] = __builtin_fma(Rc[6 + r], Rp[6 + c], __builtin_fma(Rc[3 + r], Rp[3 + c], Rc[r] * Rp[c]));
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c)
+                    Mr[r * 3 + c] = __builtin_fma(rel[r * 3 + 2], A.Kinv[6 + c],
+                                                  __builtin_fma(rel[r * 3 + 1], A.Kinv[3 + c], rel[r * 3] * A.Kinv[c]));
+            const double uf[3] = {(double)f0, (double)f1, 1.0};
+            for (int r = 0; r < 3; ++r) vp[r] = dot_c102(Mr + r * 3, uf);            // matmul output (C-order) @ v
+            double dot = vc[0] * vp[0] + vc[1] * vp[1] + vc[2] * vp[2];
+            double nc = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
+            double np = sqrt(vp[0] * vp[0] + vp[1] * vp[1] + vp[2] * vp[2]);
+            double cs = dot / (nc * np);
+            cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
+            // np.degrees(np.arccos(c)) < min_baseline_angle (:144-147) without a device acos:
+            // arccos is monotone, so the gate is c >= the smallest double the host's own
+            // np.arccos puts inside the angle (engine.baseline_cos_threshold); NaN stays false
+            tri = !(cs >= A.cos_thr);                                   // else retained
+        }
+        tacc[i] = 0;
+        if (tri) tlist[atomicAdd(&sh_m, 1)] = i;
+    }
+    __syncthreads();
+    const int m = sh_m;
+    for (int j = tid; j < m; j += blockDim.x) {
+        const int i = tlist[j];
+        const float k0 = ck[2 * i], k1 = ck[2 * i + 1], f0 = cf[2 * i], f1 = cf[2 * i + 1];
+        const int tau = ct[i];
+        const double* Rp = poseR + (int64_t)tau * 9;
+        const double* tp = poset + (int64_t)tau * 3;
+        double Rpw[9], tpw[3], Pp[12];
+        pose_inverse(Rp, tp, tau, Rpw, tpw);
+        proj_matrix(A.K, Rpw, tpw, Pp);
+        double X4[4];
+        tri_one(Pp, Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
+        const float w4 = (float)X4[3];
+        float Xo[3];
+        Xo[0] = (float)X4[0] / w4;
+        Xo[1] = (float)X4[1] / w4;
+        Xo[2] = (float)X4[2] / w4;
+        const double zc = depth_of(Rcwc, tcwc, nF, Xo);
+        const double zp = depth_of(Rpw, tpw, tau, Xo);
+        if (zc > A.min_d && zp > A.min_d && zc < A.max_d && zp < A.max_d) {
+            tacc[i] = 1;
+            tX[3 * i] = Xo[0]; tX[3 * i + 1] = Xo[1]; tX[3 * i + 2] = Xo[2];
+        }                                                               // else retained (quirk Q5)
+    }
+    __syncthreads();
     int nL = s.nL[b];
     int kept = 0;
     for (int base = 0; base < nC; base += blockDim.x) {
         const int i = base + tid;
-        bool retain = false, accept = false;
-        float k0 = 0, k1 = 0, f0 = 0, f1 = 0, Xo[3] = {0, 0, 0};
+        const int nvalid = nC - base < (int)blockDim.x ? nC - base : (int)blockDim.x;
+        const bool valid = i < nC;
+        bool accept = false;
+        float k0 = 0, k1 = 0, f0 = 0, f1 = 0;
         int tau = 0;
-        if (i < nC) {
+        if (valid) {
             k0 = ck[2 * i]; k1 = ck[2 * i + 1]; f0 = cf[2 * i]; f1 = cf[2 * i + 1]; tau = ct[i];
-            if (nF > 1 && nF - tau <= A.min_frames) {
-                retain = true;                                        // :175-178
-            } else {
-                const double* Rp = poseR + (int64_t)tau * 9;
-                const double* tp = poset + (int64_t)tau * 3;
-                // check_baseline :117-147: v_cur = K^-1 [u;1], v_past = ((R_cur^T R_past)^T K^-1) [u_f;1]
-                double vc[3], vp[3], rel[9], Mr[9];
-                const double uc[3] = {(double)k0, (double)k1, 1.0};
-                for (int r = 0; r < 3; ++r) vc[r] = dot_c102(A.Kinv + r * 3, uc);      // K_inv (C-order) @ v
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c)
-                        rel[c * 3 + r] = __builtin_fma(Rc[6 + r], Rp[6 + c], __builtin_fma(Rc[3 + r], Rp[3 + c], Rc[r] * Rp[c]));
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c)
-                        Mr[r * 3 + c] = __builtin_fma(rel[r * 3 + 2], A.Kinv[6 + c],
-                                                      __builtin_fma(rel[r * 3 + 1], A.Kinv[3 + c], rel[r * 3] * A.Kinv[c]));
-                const double uf[3] = {(double)f0, (double)f1, 1.0};
-                for (int r = 0; r < 3; ++r) vp[r] = dot_c102(Mr + r * 3, uf);            // matmul output (C-order) @ v
-                double dot = vc[0] * vp[0] + vc[1] * vp[1] + vc[2] * vp[2];
-                double nc = sqrt(vc[0] * vc[0] + vc[1] * vc[1] + vc[2] * vc[2]);
-                double np = sqrt(vp[0] * vp[0] + vp[1] * vp[1] + vp[2] * vp[2]);
-                double cs = dot / (nc * np);
-                cs = cs < -1.0 ? -1.0 : (cs > 1.0 ? 1.0 : cs);
-                // np.degrees(np.arccos(c)) < min_baseline_angle (:144-147) without a device acos:
-                // arccos is monotone, so the gate is c >= the smallest double the host's own
-                // np.arccos puts inside the angle (engine.baseline_cos_threshold); NaN stays false
-                if (cs >= A.cos_thr) {
-                    retain = true;
-                } else {
-                    double Rpw[9], tpw[3], Pp[12];
-                    pose_inverse(Rp, tp, tau, Rpw, tpw);
-                    proj_matrix(A.K, Rpw, tpw, Pp);
-                    double X4[4];
-                    tri_one(Pp, Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
-                    const float w4 = (float)X4[3];
-                    Xo[0] = (float)X4[0] / w4;
-                    Xo[1] = (float)X4[1] / w4;
-                    Xo[2] = (float)X4[2] / w4;
-                    const double zc = depth_of(Rcwc, tcwc, nF, Xo);
-                    const double zp = depth_of(Rpw, tpw, tau, Xo);
-                    if (zc > A.min_d && zp > A.min_d && zc < A.max_d && zp < A.max_d) accept = true;
-                    else retain = true;                               // quirk Q5
-                }
-            }
+            accept = tacc[i] != 0;
         }
-        int tacc, tret;
-        const int pa = nL + block_scan_flag(accept, lds, &tacc);
-        const int pr = kept + block_scan_flag(retain, lds, &tret);
+        int tacc_n;
+        const int pre = block_scan_flag(accept, lds, &tacc_n);          // every thread before tid is valid
         if (accept) {
+            const int pa = nL + pre;
             if (pa < d.ncap) {
-                X[3 * pa] = Xo[0]; X[3 * pa + 1] = Xo[1]; X[3 * pa + 2] = Xo[2];
+                X[3 * pa] = tX[3 * i]; X[3 * pa + 1] = tX[3 * i + 1]; X[3 * pa + 2] = tX[3 * i + 2];
                 kp[2 * pa] = k0; kp[2 * pa + 1] = k1;
             } else {
                 sh_fail = 1;
             }
-        }
-        if (retain) {
+        } else if (valid) {
+            const int pr = kept + (tid - pre);
             ck[2 * pr] = k0; ck[2 * pr + 1] = k1; cf[2 * pr] = f0; cf[2 * pr + 1] = f1; ct[pr] = tau;
         }
-        nL += tacc;
-        kept += tret;
+        nL += tacc_n;
+        kept += nvalid - tacc_n;
         __syncthreads();
     }
     if (tid == 0) {
@@ -868,7 +922,9 @@ k_pnp_tri(PnPArgs A, TriArgs T)
     __syncthreads();
     pnp_apply_block(T.d, T.s, A.rvec, A.tvec, A.success, A.mask);
     __syncthreads();
+    PNPPROF(14);
     triangulate_block(T);
+    PNPPROF(15);
 }
 
 // ------------------------------------------------ feature adding + step finish
@@ -1122,6 +1178,20 @@ extern "C" int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const v
     A.min_dist = o->feature_min_dist;
     A.boot = 0;
     hipLaunchKernelGGL(k_add_finish, dim3(d->B), dim3(ADD_THREADS), 0, VO_STREAM(stream), A);
+    return hip_rc();
+}
+
+namespace {
+__global__ void k_status_word(const int32_t* status, const int32_t* n_inl, int32_t* dst)
+{
+    if (threadIdx.x == 0) { dst[0] = status[0]; dst[1] = n_inl[0]; }
+}
+}  // namespace
+
+extern "C" int vo_status_word(const vo_state* s, int32_t* dst, vo_stream_t stream)
+{
+    if (!s || !dst) return VO_EARG;
+    hipLaunchKernelGGL(k_status_word, dim3(1), dim3(64), 0, VO_STREAM(stream), s->status, s->nInl, dst);
     return hip_rc();
 }
 
