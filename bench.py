@@ -365,10 +365,12 @@ def gpu_chain_positions(K, opts, frames_dev, device):
     eng.bootstrap(frames_dev[0:1], frames_dev[1:2])
     torch.cuda.synchronize()
     lat = []
+    # per frame exactly what the drop-in class does (VisualOdometryPipeLine.continuous_operation):
+    # the step, then the chain's status word into pinned memory and one stream synchronisation
     for i in range(2, frames_dev.shape[0]):
         t0 = time.perf_counter()
         eng.step(frames_dev[i:i + 1])
-        torch.cuda.synchronize()
+        eng.status_word()
         lat.append(time.perf_counter() - t0)
     ex = eng.export_chain(0)
     pos = np.array([np.asarray(t).ravel() for _, t in ex["transforms"]])
@@ -383,7 +385,7 @@ def gpu_chain_positions(K, opts, frames_dev, device):
     for i in range(2, frames_dev.shape[0]):
         t0 = time.perf_counter()
         eng2.step_graph(frames_dev[i:i + 1])
-        torch.cuda.synchronize()
+        eng2.status_word(in_graph=True)
         lat_g.append(time.perf_counter() - t0)
     pos_g = np.array([np.asarray(t).ravel() for _, t in eng2.export_chain(0)["transforms"]])
     same = pos_g.shape == pos.shape and bool(np.array_equal(pos_g, pos))

@@ -284,7 +284,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
     if (wave_id() == 0)
         wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp);
     __syncthreads();
-    if (tid == 0) for (int j = 0; j < 3; ++j) S.cws[0][j] = S.tmp[j] / n;
+    if (tid == 0) for (int j = 0; j < 3; ++j) S.pw0[j] = S.cws[0][j] = S.tmp[j] / n;
     __syncthreads();
     if (wave_id() == 0)
         wave_det_sum<9>(n, [&](int i, double* c) {
@@ -394,12 +394,9 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
     __syncthreads();
     PNPPROF(12);
     // the oracle runs approximation 1's R,t before computing approximation 2's betas; the
-    // betas do not depend on R,t, so computing all betas first is equivalent
-    if (wave_id() == 0)
-        wave_det_sum<3>(n, [&](int i, double* c) { c[0] = pws[3 * i]; c[1] = pws[3 * i + 1]; c[2] = pws[3 * i + 2]; }, S.tmp + 72);
-    __syncthreads();
-    if (tid == 0) for (int j = 0; j < 3; ++j) S.pw0[j] = S.tmp[72 + j] / n;
-    __syncthreads();
+    // betas do not depend on R,t, so computing all betas first is equivalent.  compute_R_and_t's
+    // world centroid pw0 is the same sum of the same points in the same order as the first
+    // control point cws[0] (set with it above), so it is not summed again.
     if (wave_id() < 3) epnp_R_and_t_wave(S, wave_id() + 1, K, pws, us, alphas, n);
     __syncthreads();
     PNPPROF(13);

@@ -335,7 +335,12 @@ class Engine:
         frames are copied into the graph's bound input buffer first)."""
         if not self._graphs:
             self.capture_step()
-        self._graphs["buf"].copy_(self._frames(frames))
+        buf = self._graphs["buf"]
+        if (isinstance(frames, torch.Tensor) and frames.dtype == torch.uint8 and frames.shape == buf.shape
+                and frames.device == buf.device):
+            buf.copy_(frames)                       # device frames: no host-side checks / staging
+        else:
+            buf.copy_(self._frames(frames))
         self.replay_step()
 
     # ------------------------------------------------------------------ bootstrap
