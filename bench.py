@@ -451,6 +451,8 @@ def main():
             e.bootstrap(frames[0, bounds[g]:bounds[g + 1]], frames[1, bounds[g]:bounds[g + 1]])
     torch.cuda.synchronize()
     boot_s = time.perf_counter() - t0
+    for e in engines:
+        e.release_bootstrap()                     # 64 GB per engine; the later legs bootstrap their own
 
     def step_all(j, marks=None):
         for g, e in enumerate(engines):

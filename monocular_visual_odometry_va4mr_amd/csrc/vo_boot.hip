@@ -307,7 +307,13 @@ struct EssArgs {
     const int32_t* chain_status;
 };
 
-__global__ void __launch_bounds__(256) k_essential(EssArgs A)
+// WPE 2: the build for more chains than CUs (at most 256 registers per lane, two blocks per CU;
+// 768-chain bootstrap 0.365 vs 0.368-0.404 s).  Scoring is in the sequential rule's order, one
+// hypothesis per wave per batch, and stops at the running adaptive count (identical result to
+// scoring all EHYP).  Measured and not kept: the five-point solves spread over 16 lanes of each
+// wave instead of one whole wave (0.376 s).
+template <int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_essential(EssArgs A)
 {
     __shared__ int sub[EHYP][5];
     __shared__ int nmod[EHYP];
@@ -384,34 +390,40 @@ __global__ void __launch_bounds__(256) k_essential(EssArgs A)
         __syncthreads();
         {
             const int w = wave_id(), lane = lane_id(), nw = blockDim.x >> 6;
-            for (int h = w; h < EHYP; h += nw)
-                for (int m = 0; m < nmod[h]; ++m) {
-                    const double* Em = models + 90 * h + 9 * m;
-                    int c = 0;
-                    for (int i = lane; i < n; i += 64)
-                        c += sampson_err(Em, q1[2 * i], q1[2 * i + 1], q2[2 * i], q2[2 * i + 1]) <= thr;
-                    c = wave_sum_i32(c);
-                    if (lane == 0) cnt[h][m] = c;
-                }
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int niters = sh[1], best = sh[2];
-            for (int h = 0; h < EHYP; ++h) {
-                if (it0 + h >= niters) break;
-                for (int m = 0; m < nmod[h]; ++m) {
-                    const int good = cnt[h][m];
-                    if (good > (best > 4 ? best : 4)) {
-                        best = good;
-                        for (int q = 0; q < 9; ++q) bestE[q] = models[90 * h + 9 * m + q];
-                        niters = ransac_update_niters(A.prob, (double)(n - good) / n, 5, niters);
+            for (int h0 = 0; h0 < EHYP; h0 += nw) {
+                if (it0 + h0 >= sh[1]) break;                                 // block-uniform
+                const int h = h0 + w;
+                if (h < EHYP)
+                    for (int m = 0; m < nmod[h]; ++m) {
+                        const double* Em = models + 90 * h + 9 * m;
+                        int c = 0;
+                        for (int i = lane; i < n; i += 64)
+                            c += sampson_err(Em, q1[2 * i], q1[2 * i + 1], q2[2 * i], q2[2 * i + 1]) <= thr;
+                        c = wave_sum_i32(c);
+                        if (lane == 0) cnt[h][m] = c;
                     }
+                __syncthreads();
+                if (tid == 0) {
+                    int niters = sh[1], best = sh[2];
+                    const int h1 = h0 + nw < EHYP ? h0 + nw : EHYP;
+                    for (int hh = h0; hh < h1; ++hh) {
+                        if (it0 + hh >= niters) break;
+                        for (int m = 0; m < nmod[hh]; ++m) {
+                            const int good = cnt[hh][m];
+                            if (good > (best > 4 ? best : 4)) {
+                                best = good;
+                                for (int q = 0; q < 9; ++q) bestE[q] = models[90 * hh + 9 * m + q];
+                                niters = ransac_update_niters(A.prob, (double)(n - good) / n, 5, niters);
+                            }
+                        }
+                    }
+                    sh[1] = niters;
+                    sh[2] = best;
                 }
+                __syncthreads();
             }
-            sh[0] = it0 + EHYP;
-            sh[1] = niters;
-            sh[2] = best;
         }
+        if (tid == 0) sh[0] = it0 + EHYP;
         __syncthreads();
     }
     const bool ok = sh[2] > 0;
@@ -615,6 +627,13 @@ static void fill_ess(EssArgs& A, const vo_opts* o, const float* p0, const float*
     A.work = work; A.work_stride = ws; A.E = E; A.mask = mask; A.ok = ok; A.chain_status = st;
 }
 
+static void launch_essential(const EssArgs& A, int B, hipStream_t st)
+{
+    const int n_cu = device_cus() > 0 ? device_cus() : 256;          // of the current device
+    if (B > n_cu) hipLaunchKernelGGL(k_essential<2>, dim3(B), dim3(256), 0, st, A);
+    else hipLaunchKernelGGL(k_essential<1>, dim3(B), dim3(256), 0, st, A);
+}
+
 extern "C" int vo_find_essential(const vo_opts* o, int B, const float* p0, const float* p1, const int32_t* counts,
                                  int32_t cap, double prob, double threshold, int32_t max_iters, double* E,
                                  uint8_t* mask, int32_t* ok, double* work, int32_t work_doubles, vo_stream_t stream)
@@ -623,7 +642,7 @@ extern "C" int vo_find_essential(const vo_opts* o, int B, const float* p0, const
     if ((int64_t)work_doubles < 4LL * cap + 90 * EHYP) return VO_EARG;
     EssArgs A;
     fill_ess(A, o, p0, p1, counts, cap, prob, threshold, max_iters, E, mask, ok, work, work_doubles, nullptr);
-    hipLaunchKernelGGL(k_essential, dim3(B), dim3(256), 0, VO_STREAM(stream), A);
+    launch_essential(A, B, VO_STREAM(stream));
     return hip_rc();
 }
 
@@ -660,7 +679,7 @@ extern "C" int vo_bootstrap(const vo_dims* d, const vo_opts* o, const vo_state* 
     if (cap > d->ncap) return VO_EARG;            // the E mask lives in pnp_mask [B][ncap]
     A.mask = s->pnp_mask;
     A.cap = cap;
-    hipLaunchKernelGGL(k_essential, dim3(d->B), dim3(256), 0, st, A);
+    launch_essential(A, d->B, st);
     hipLaunchKernelGGL(k_boot_apply, dim3(d->B), dim3(256), 0, st, *d, *s, pts0, pts1, counts, cap,
                        (const uint8_t*)s->pnp_mask, (const int32_t*)s->pnp_ok);
     RecArgs Rg;

@@ -354,7 +354,7 @@ class Engine:
         VisualOdometryPipeLine.py:35 is likewise done once, in the constructor); bootstrap()
         calls it itself when nothing is reserved.  Returns (Sift, chains per chunk)."""
         from .features import Sift
-        budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 24 << 30))
+        budget = int(sift_batch_bytes or os.environ.get("VO_SIFT_BATCH_BYTES", 64 << 30))
         per_img = Sift.bytes_per_image(self.W, self.H)
         m = max(1, min(self.B, budget // (2 * per_img)))     # chains per chunk
         nfeat = int(self.options.get("sift_nfeatures", 0))    # C5: SIFT_create(8192)
@@ -364,6 +364,11 @@ class Engine:
             self._sift = Sift(self.W, self.H, self.device, batch=2 * m, nfeatures=nfeat)
         return self._sift, m
 
+    def release_bootstrap(self):
+        """Free the SIFT workspace (stepping never needs it)."""
+        self._sift = None
+        torch.cuda.empty_cache()
+
     def bootstrap(self, img0, img1, sift_batch_bytes: int | None = None):
         """initialization (VisualOdometryPipeLine.py:293-323) for every chain on the GPU:
         SIFT on both frames, BF 2-NN + ratio test, 5-point E-RANSAC, inlier split,
@@ -372,7 +377,7 @@ class Engine:
         preset's 8192) is SIFT_create(nfeatures).
 
         Batched across chains: the chains are taken in chunks whose SIFT scale spaces fit
-        ``sift_batch_bytes`` (default 24 GB, env VO_SIFT_BATCH_BYTES); per chunk one
+        ``sift_batch_bytes`` (default 64 GB, env VO_SIFT_BATCH_BYTES); per chunk one
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync until
         the SIFT capacity check, which comes before any chain state is written."""
