@@ -379,8 +379,8 @@ class Engine:
         Batched across chains: the chains are taken in chunks whose SIFT scale spaces fit
         ``sift_batch_bytes`` (default 64 GB, env VO_SIFT_BATCH_BYTES); per chunk one
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
-        and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync until
-        the SIFT capacity check, which comes before any chain state is written."""
+        and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync: a chain
+        whose SIFT keypoints hit the capacity ends with status VO_ST_CAPACITY."""
         from .features import bf_knn2_batch
         img0 = self._frames(img0)
         img1 = self._frames(img1)
@@ -395,13 +395,14 @@ class Engine:
         cnt = torch.zeros(B, dtype=torch.int32, device=dev)
         n0 = torch.zeros(B, dtype=torch.int32, device=dev)
         n1 = torch.zeros_like(n0)
-        overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+        ovf = torch.zeros(B, dtype=torch.int32, device=dev)      # per chain: SIFT capacity hit
         st = self.stream
         for c0 in range(0, B, m):
             c1 = min(B, c0 + m)
             k = c1 - c0
             kp, desc, n = sift.run_batch(torch.cat([img0[c0:c1], img1[c0:c1]]))
-            overflow = torch.maximum(overflow, sift.t["counters"][:2 * k, 3].max().reshape(1))
+            flag = sift.t["counters"][:2 * k, 3]
+            ovf[c0:c1] = torch.maximum(flag[:k], flag[k:])
             n0[c0:c1] = n[:k]
             n1[c0:c1] = n[k:]
             idx2, dist2 = bf_knn2_batch(desc[:k], n[:k], desc[k:], n[k:])
@@ -410,13 +411,13 @@ class Engine:
                                                 C.c_void_p(n[:k].data_ptr()), kcap, float(self.opts.feature_ratio),
                                                 C.c_void_p(pts0[c0:c1].data_ptr()), C.c_void_p(pts1[c0:c1].data_ptr()),
                                                 C.c_void_p(cnt[c0:c1].data_ptr()), cap, st), "vo_ratio_matches")
-        # one host sync before any chain state is touched: a truncated keypoint or match set
-        # must not bootstrap a chain
-        if int(overflow):
-            raise RuntimeError("SIFT capacity exceeded")
         self._chk(self.lib.vo_bootstrap(self._pd, self._po, self._ps, C.c_void_p(pts0.data_ptr()),
                                         C.c_void_p(pts1.data_ptr()), C.c_void_p(cnt.data_ptr()), cap, st),
                   "vo_bootstrap")
+        # a chain whose keypoint set was truncated by the SIFT capacity must not run on: its status
+        # becomes VO_ST_CAPACITY on the device (every stage skips it, statuses() / the drop-in
+        # class report it) -- no host synchronisation inside the bootstrap
+        self.t["status"].copy_(torch.where(ovf > 0, torch.full_like(ovf, L.ST_CAPACITY), self.t["status"]))
         self.prev = 0
         self.build_pyramid(img1, self.prev)
         self._boot_debug = {"n0": n0, "n1": n1, "pts0": pts0, "pts1": pts1, "cnt": cnt}
