@@ -93,8 +93,11 @@ class VisualOdometryPipeLine:
             eng.step(img[None])
         self._frame = img
         st, n_inl = eng.status_word(in_graph=self._use_graph)  # one host sync per frame
-        if st == L.ST_OK:
-            if len(self.num_tracked_landmarks_list) == 20:     # :360-364
+        # the reference appends to the ring (:360-364) after PnP succeeded and before
+        # feature_adding (:369), so a frame that then crashes in goodFeaturesToTrack (:256)
+        # has already appended its inlier count
+        if st in (L.ST_OK, L.ST_GFTT_NONE, L.ST_GFTT_ONE):
+            if len(self.num_tracked_landmarks_list) == 20:
                 self.num_tracked_landmarks_list.pop(0)
             self.num_tracked_landmarks_list.append(n_inl)
         self._raise_status(st)

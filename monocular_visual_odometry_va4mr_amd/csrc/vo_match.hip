@@ -216,19 +216,23 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 // |q - t|^2 = |q'|^2 + |t'|^2 - 2 q'.t' with q' = q - 128, t' = t - 128 (the distance is
 // shift-invariant); v_mfma_i32_32x32x32_i8 forms q'.t' exactly in int32 at twice the bf16 rate.
 // The lane keeps the running top-2 of s = 2 q'.t' - |t'|^2 (= |q'|^2 - d^2), as k_bf_mfma does.
-// With |t'|^2 = 2h + p (p = parity) the MFMA accumulator starts at -h, so it ends at
-// a = q'.t' - h and s = 2a - p: s orders as (a descending, p ascending), every s <= 2a, and the
-// per-candidate work is one v_max3 per two candidates plus one test against the lane's
-// second-best; only candidates that may enter (2 max(a) > s1, rare) form s exactly.
+// (cv2compat.knnMatch rejects values outside 0..255, which would wrap in the int8 encoding.)
 //
-//  k_bf_prep_i8  descriptors -> int8 rows (v - 128) + centered squared norms |v'|^2; eight
+//  k_bf_prep_i8  descriptors -> int8 rows (v - 128) + centred squared norms |v'|^2; eight
 //                threads per row, 16 values each (four float4 loads, one 16-byte store)
-//  k_bf_i8       block = 4 waves x 32 queries; 64-row int8 train tiles double-buffered in LDS
-//                (16-B slots XOR-swizzled by row); per tile each wave runs 2 x 4 MFMAs (two
-//                32-row sub-tiles, interleaved) with the train rows as A and its queries as B.
-//                Lane (r, g) supplies bytes 16g..16g+15 of every 32-byte K chunk for both
-//                operands: the same k for the same (g, element) on both sides, so the MFMA sums
-//                every k of the chunk once whatever the hardware's k order inside a chunk.
+//  k_bf_i8       block = 4 waves x 32 queries; TT = 128-row int8 train tiles double-buffered in
+//                LDS (16-B slots swizzled by (row >> 1) & 7), the next tile prefetched by buffer
+//                loads during the MFMAs.  Per 32-row sub-tile a wave runs 4 MFMAs (one per
+//                32-byte K chunk) with the train rows as A and its queries as B; the next
+//                sub-tile's MFMAs are issued before this one's epilogue.  Lane (r, g) supplies
+//                bytes 16g..16g+15 of every 32-byte K chunk for both operands: the same k for the
+//                same (g, element) on both sides, so the MFMA sums every k of the chunk once
+//                whatever the hardware's k order inside a chunk.
+//                Epilogue: key = (acc << 5) + 16 (-|t'|^2) + (15 - reg) = 16 s + (15 - reg) per
+//                accumulator register (the staged ntn row term), so the largest key is the
+//                largest s with ties to the lowest train index of the lane; the sub-tile's two
+//                largest keys come from four v_max / v_med3 running top-2 chains merged pairwise,
+//                and only they are tested against the lane's running second-best.
 __global__ void __launch_bounds__(256) k_bf_prep_i8(const float* __restrict__ src, const int32_t* n, int B, int cap,
                                                     int8_t* __restrict__ dst, int32_t* __restrict__ nrm)
 {

@@ -276,6 +276,10 @@ class _BFMatcher:
             raise NotImplementedError("128-D float descriptors (SIFT)")
         if not (np.array_equal(q, np.round(q)) and np.array_equal(t, np.round(t))):
             raise NotImplementedError("the MFMA matcher is exact for integer-valued (SIFT) descriptors")
+        # the int8 kernel stores v - 128: exact for 0..255 (SIFT's saturate_cast<uchar> range),
+        # anything outside would wrap into a wrong distance
+        if (q.size and (q.min() < 0 or q.max() > 255)) or (t.size and (t.min() < 0 or t.max() > 255)):
+            raise NotImplementedError("the MFMA matcher takes descriptor values 0..255 (SIFT)")
         dev = _dev()
         nq, nt = q.shape[0], t.shape[0]
         if nq == 0:

@@ -387,6 +387,9 @@ class Engine:
         d = self.dims
         dev = self.device
         B = self.B
+        # a workspace the caller reserved stays (reserve_bootstrap / release_bootstrap); one
+        # allocated here is freed at the end, so stepping never holds up to the SIFT budget
+        own = getattr(self, "_sift", None) is None
         sift, m = self.reserve_bootstrap(sift_batch_bytes)
         kcap = sift.kp_cap
         cap = min(d.ncap, d.pcap, kcap)
@@ -421,6 +424,10 @@ class Engine:
         self.prev = 0
         self.build_pyramid(img1, self.prev)
         self._boot_debug = {"n0": n0, "n1": n1, "pts0": pts0, "pts1": pts1, "cnt": cnt}
+        if own:
+            # the caching allocator only reuses the blocks once the queued kernels are done
+            # with them; dropping the references is stream-ordered, so no synchronisation
+            self._sift = None
 
     # ------------------------------------------------------------------ state I/O
     def import_chain(self, b: int, *, landmarks, keypoints, cand, cand_first, cand_tau, transforms,

@@ -35,9 +35,25 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def default_groups(chains: int) -> int:
+    """Stream groups for a rank's chains (run's ``groups``): one engine up to 16 chains
+    (latency-bound: a second stream only adds a queue hop), two above (measured,
+    tools/seq_sweep.py)."""
+    return 1 if chains <= 16 else 2
+
+
 def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, seed: int = 1, device=None,
         rank: int = 0, world: int = 1, out_path: str | None = None, engine_cls=None, renderer=None,
-        reference: dict | None = None, prerender: bool = True, time_boot: bool = True) -> dict | None:
+        reference: dict | None = None, prerender: bool = True, time_boot: bool = True,
+        groups: int | None = None) -> dict | None:
     """Run the plan; rank 0 returns the report (None on other ranks).
 
     ``engine_cls`` / ``renderer`` default to engine.Engine and synth.Renderer (tests pass
@@ -45,7 +61,11 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     shard index to the reference CPU trajectory of that shard (positions [n, 3]).  With
     ``prerender`` the rank's frames are rendered into device memory before the clock starts;
     ``wall`` then covers bootstrap + every step (one host sync at the end, plus one after the
-    bootstrap when ``time_boot``)."""
+    bootstrap when ``time_boot``).
+
+    ``groups``: the rank's chains are split into this many engines, each on its own HIP
+    stream, so that one group's latency-bound stages (PnP, GFTT selection: a block per chain)
+    run while another group's tracking fills the GPU (default: ``default_groups(B)``)."""
     dev = torch.device(device or "cuda")
     if engine_cls is None:
         from .engine import Engine as engine_cls
@@ -60,20 +80,31 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     B = len(mine)
     Rs, cs = poses(n_frames, renderer.p)
     max_f = max(s.end - s.boot1 + 1 for s in plan)
-    eng = engine_cls(renderer.K, opts, renderer.W, renderer.H, batch=B, device=dev, ncap=16384, pcap=16384,
-                     fcap=max_f + 8)
+    G = max(1, min(B, default_groups(B) if groups is None else int(groups)))
+    bounds = [(g * B) // G for g in range(G + 1)]
+    cuda = dev.type == "cuda"
+    engines = [engine_cls(renderer.K, opts, renderer.W, renderer.H, batch=bounds[g + 1] - bounds[g], device=dev,
+                          ncap=16384, pcap=16384, fcap=max_f + 8) for g in range(G)]
+    streams = [torch.cuda.Stream(dev) if cuda and G > 1 else None for _ in range(G)]
 
     n_steps = max(s.n_steps for s in mine)
     lo = min(s.start for s in mine)
     hi = min(n_frames, max(s.end for s in mine))
-    cache = None
+    # frame of chain b at step j: its own next frame, or its last one again once its shard has
+    # ended (what the padded chain does then does not count, see final_status below)
+    idx = np.array([[min(s.boot1 + 1 + j, s.end - 1, n_frames - 1) for s in mine] for j in range(n_steps)],
+                   np.int64).reshape(n_steps, B)
+    cache = idx_dev = None
     if prerender:
         # every frame of this rank's shards rendered into HBM before the clock starts (the
-        # workload is the VO, not the renderer); ~0.47 MB per KITTI frame
+        # workload is the VO, not the renderer); ~0.47 MB per KITTI frame.  The per-step frame
+        # indices go to the device once too: no host-to-device copy (and so no implicit
+        # synchronisation) inside the stepping loop
         cache = torch.empty((hi - lo, renderer.H, renderer.W), dtype=torch.uint8, device=dev)
         for a in range(lo, hi, 32):
             b = min(hi, a + 32)
             cache[a - lo:b - lo] = renderer.render_batch(list(range(a, b)), Rs[a:b], cs[a:b])
+        idx_dev = torch.from_numpy(idx - lo).to(dev)
 
     def frames_at(ids):
         ids = [min(int(i), n_frames - 1) for i in ids]
@@ -81,26 +112,57 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
             return cache[torch.as_tensor([i - lo for i in ids], device=dev)]
         return renderer.render_batch(ids, Rs[ids], cs[ids])
 
+    def step_frames(j, g):
+        if idx_dev is not None:
+            return cache.index_select(0, idx_dev[j, bounds[g]:bounds[g + 1]])
+        return frames_at(idx[j, bounds[g]:bounds[g + 1]])
+
+    def on(g):
+        return torch.cuda.stream(streams[g]) if streams[g] is not None else _nullctx()
+
+    boot0 = frames_at([s.start for s in mine])
+    boot1 = frames_at([s.boot1 for s in mine])
+    last = np.array([s.n_steps - 1 for s in mine])
+    last_dev = [torch.as_tensor(last[bounds[g]:bounds[g + 1]], device=dev) for g in range(G)]
     _sync(dev)
     t0 = time.perf_counter()
-    eng.bootstrap(frames_at([s.start for s in mine]), frames_at([s.boot1 for s in mine]))
+    if G > 1 and cuda:
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream(dev))
+    for g, eng in enumerate(engines):
+        with on(g):
+            eng.bootstrap(boot0[bounds[g]:bounds[g + 1]], boot1[bounds[g]:bounds[g + 1]])
     if time_boot:
         _sync(dev)
     t_boot = time.perf_counter() - t0
     # status of every chain at its shard's own last step (chains whose shard has ended keep
     # re-reading their last frame until the longest shard is done; what happens to them then
     # does not count; a shard with no step keeps its bootstrap status, the clone below).
-    # Kept on the device: no host sync inside the loop.
-    last_step = torch.tensor([s.n_steps - 1 for s in mine], device=dev)
-    final_status = eng.t["status"].clone()
+    # Kept on the device, and updated only at the steps where some shard ends.
+    final_status = []
+    for g, eng in enumerate(engines):
+        with on(g):
+            final_status.append(eng.t["status"].clone())
+    ends = {}
+    for g in range(G):
+        for j in set(int(v) for v in last[bounds[g]:bounds[g + 1]] if v >= 0):
+            ends.setdefault(j, []).append(g)
     for j in range(n_steps):
-        eng.step(frames_at([min(s.boot1 + 1 + j, s.end - 1) for s in mine]))
-        final_status = torch.where(last_step == j, eng.t["status"], final_status)
+        for g, eng in enumerate(engines):
+            with on(g):
+                eng.step(step_frames(j, g))
+                if g in ends.get(j, ()):
+                    final_status[g] = torch.where(last_dev[g] == j, eng.t["status"], final_status[g])
+    if G > 1 and cuda:
+        for st in streams:
+            torch.cuda.current_stream(dev).wait_stream(st)
+    host_s = time.perf_counter() - t0
     _sync(dev)
     wall = time.perf_counter() - t0
     t_step = wall - t_boot
+    final_status = torch.cat(final_status)
     t_g = time.perf_counter()
-    packed = Sh.pack_poses(eng.t["pose_R"], eng.t["pose_t"], eng.t["nF"], eng.dims.fcap)
+    packed = torch.cat([Sh.pack_poses(e.t["pose_R"], e.t["pose_t"], e.t["nF"], e.dims.fcap) for e in engines])
     allp = Sh.gather_poses(packed)
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
@@ -137,7 +199,8 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
         "shard_status": {str(int(k)): int(v) for k, v in zip(*np.unique(statuses, return_counts=True))},
         "sequence_frames_per_s": round(n_frames / max(wall, 1e-9), 1),
         "step_frames_per_s": round(frames_done / max(t_step, 1e-9), 1),
-        "wall_s": round(wall, 3), "bootstrap_s": round(t_boot, 3), "step_s": round(t_step, 3),
+        "wall_s": round(wall, 4), "bootstrap_s": round(t_boot, 4), "step_s": round(t_step, 4),
+        "steps": n_steps, "groups": G, "host_launch_s": round(host_s, 4),
         # after the clock: pose gather (the collective) and the Sim(3) stitch on rank 0
         "gather_ms": round(t_gather * 1e3, 3), "stitch_ms": round(t_stitch * 1e3, 3),
         "job_frames_per_s": round(n_frames / max(wall + t_gather + t_stitch, 1e-9), 1),

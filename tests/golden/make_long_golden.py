@@ -9,10 +9,14 @@ KITTI-length synthetic C2 sequence (4541 frames, seed 1):
   kitti_seq00_shards.npz  the same sequence cut by shards.plan_shards into 8 (C4: one
                           shard per GPU) and 16 shards (two per GPU / one GPU), each shard
                           run by its own reference instance on its own boundaries (§8e)
+  kitti_seq00_shards_wide.npz  the wider cuts of the sequence job (shards per GPU as the batch
+                          dimension, n_shards = world x B_seq): --cuts 32,64,... --no-full
+                          --out kitti_seq00_shards_wide.npz (keys of cuts already in the
+                          file are kept, new cuts are added)
 
 Frames are rendered once into a raw memmap (every frame's SHA-1 is stored, so the GPU
 tests can check their own renders), then the reference runs are spread over processes.
-Usage:  python tests/golden/make_long_golden.py [--procs 8]
+Usage:  python tests/golden/make_long_golden.py [--procs 8] [--cuts 8,16] [--no-full] [--out FILE]
 """
 from __future__ import annotations
 
@@ -33,6 +37,7 @@ PRESET, SEED, N_FRAMES = "kitti", 1, 4541
 SHARD_COUNTS = (8, 16)
 OVERLAP = 30
 MEMMAP = "/tmp/vo_long_golden_frames.u8"
+CACHE = "/tmp/vo_long_golden_runs"
 
 
 def _render_chunk(args):
@@ -53,6 +58,10 @@ def _render_chunk(args):
 def _run_ref(args):
     """One reference instance over frames [start] + [boot1 .. end)."""
     tag, start, boot1, end, shape = args
+    cached = os.path.join(CACHE, f"{tag}_{start}_{boot1}_{end}.npz")
+    if os.path.exists(cached):          # a resumed run (results of finished shards are kept)
+        c = np.load(cached, allow_pickle=False)
+        return tag, c["t"], c["cnt"], str(c["err"])
     import oracle.cv2_oracle as cv2_oracle
     sys.modules["cv2"] = cv2_oracle
     sys.path.insert(0, "/root/reference")
@@ -78,13 +87,20 @@ def _run_ref(args):
     t = np.stack([r[0] for r in rows])
     cnt = np.array([r[1:] for r in rows], np.int64)
     print(f"  {tag} [{start},{end}): {len(rows)} poses in {time.time() - t0:.0f}s {err}", flush=True)
+    os.makedirs(CACHE, exist_ok=True)
+    np.savez(cached + ".tmp.npz", t=t, cnt=cnt, err=np.asarray(err))
+    os.replace(cached + ".tmp.npz", cached)
     return tag, t, cnt, err
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--cuts", default=",".join(str(c) for c in SHARD_COUNTS), help="shard counts")
+    ap.add_argument("--no-full", action="store_true", help="skip the one-chain run (kitti_seq00.npz)")
+    ap.add_argument("--out", default="kitti_seq00_shards.npz", help="shard fixture file (merged)")
     a = ap.parse_args()
+    cuts = [int(c) for c in a.cuts.split(",") if c]
     from monocular_visual_odometry_va4mr_amd import options as O
     from monocular_visual_odometry_va4mr_amd import shards as Sh
     from monocular_visual_odometry_va4mr_amd.synth import SIZES
@@ -104,19 +120,27 @@ def main():
                         for i in range(N_FRAMES)])
     _, (b0, b1), _ = O.get(PRESET)
     gap = b1 - b0
-    jobs = [("full", 0, gap, N_FRAMES, shape)]
-    plans = {S: Sh.plan_shards(N_FRAMES, S, gap, OVERLAP) for S in SHARD_COUNTS}
+    jobs = [] if a.no_full else [("full", 0, gap, N_FRAMES, shape)]
+    plans = {S: Sh.plan_shards(N_FRAMES, S, gap, OVERLAP) for S in cuts}
     for S, plan in plans.items():
         jobs += [(f"s{S}_{s.index}", s.start, s.boot1, s.end, shape) for s in plan]
+    # longest runs first so the pool's tail is short
+    jobs.sort(key=lambda j: -(j[3] - j[2]))
     res = {}
     with mp.get_context("fork").Pool(a.procs) as pool:
         for tag, t, cnt, err in pool.imap_unordered(_run_ref, jobs):
             res[tag] = (t, cnt, err)
-    full_t, full_cnt, full_err = res["full"]
-    np.savez_compressed(os.path.join(HERE, "kitti_seq00.npz"), preset=PRESET, seed=SEED, n_frames=N_FRAMES,
-                        boot=np.array([b0, b1]), t=full_t, num_pts=full_cnt[:, 0], N=full_cnt[:, 1],
-                        P=full_cnt[:, 2], error=np.asarray(full_err), digests=digests)
+    full_err, full_t = "", []
+    if not a.no_full:
+        full_t, full_cnt, full_err = res["full"]
+        np.savez_compressed(os.path.join(HERE, "kitti_seq00.npz"), preset=PRESET, seed=SEED, n_frames=N_FRAMES,
+                            boot=np.array([b0, b1]), t=full_t, num_pts=full_cnt[:, 0], N=full_cnt[:, 1],
+                            P=full_cnt[:, 2], error=np.asarray(full_err), digests=digests)
+    out_path = os.path.join(HERE, a.out)
     out = {"preset": PRESET, "seed": SEED, "n_frames": N_FRAMES, "overlap": OVERLAP}
+    if os.path.exists(out_path):
+        old = np.load(out_path, allow_pickle=False)
+        out.update({k: old[k] for k in old.files if k.startswith("s") and k.split("_")[0][1:].isdigit()})
     for S, plan in plans.items():
         ts, offs, errs, cnts = [], [0], [], []
         for s in plan:
@@ -127,10 +151,10 @@ def main():
             errs.append(err)
         out[f"s{S}_bounds"] = np.array([[s.start, s.boot1, s.end] for s in plan])
         out[f"s{S}_t"] = np.concatenate(ts)
-        out[f"s{S}_counts"] = np.concatenate(cnts)
+        out[f"s{S}_counts"] = np.concatenate(cnts).astype(np.int32)
         out[f"s{S}_off"] = np.array(offs)
         out[f"s{S}_error"] = np.array(errs)
-    np.savez_compressed(os.path.join(HERE, "kitti_seq00_shards.npz"), **out)
+    np.savez_compressed(out_path, **out)
     print(f"done in {time.time() - t0:.0f}s; full chain: {len(full_t)} poses, error={full_err!r}")
 
 

@@ -94,3 +94,41 @@ def test_synth_is_deterministic_and_textured():
     assert np.array_equal(a, b) and a.dtype == np.uint8 and a.shape == (2, 480, 640)
     assert a.std() > 15
     assert np.allclose(c[1] - c[0], [0, 0, 1], atol=0.01)
+
+
+class _StatusEngine:
+    """Stand-in for a one-chain Engine that only reports a scripted (status, inliers) per frame."""
+
+    def __init__(self, script):
+        self.script = list(script)
+
+    def step(self, frames):
+        pass
+
+    step_graph = step
+
+    def status_word(self, in_graph=False):
+        return self.script.pop(0)
+
+
+@pytest.mark.parametrize("crash,exc", [(L.ST_GFTT_NONE, AttributeError), (L.ST_GFTT_ONE, IndexError),
+                                       (L.ST_NOT_ENOUGH_KP, ValueError), (L.ST_PNP_FAILED, ValueError)])
+def test_dropin_ring_appends_before_feature_adding_crash(crash, exc):
+    """VisualOdometryPipeLine.py:360-369: the 20-entry ring gets the frame's inlier count after
+    PnP succeeded and before feature_adding, so a goodFeaturesToTrack crash (:256) leaves it
+    appended; a PnP failure (:352, :358) raises before the ring is touched."""
+    from monocular_visual_odometry_va4mr_amd.VisualOdometryPipeLine import VisualOdometryPipeLine
+    from monocular_visual_odometry_va4mr_amd import options as O
+    opts, _, _ = O.get("kitti")
+    vo = VisualOdometryPipeLine(np.eye(3), opts)
+    script = [(L.ST_OK, 100 + i) for i in range(22)] + [(crash, 77)]
+    vo._eng = _StatusEngine(script)
+    vo._boot_done = True
+    img = np.zeros((4, 4), np.uint8)
+    for _ in range(22):
+        vo.continuous_operation(img)
+    assert vo.num_tracked_landmarks_list == list(range(102, 122))
+    with pytest.raises(exc):
+        vo.continuous_operation(img)
+    appended = crash in (L.ST_GFTT_NONE, L.ST_GFTT_ONE)
+    assert vo.num_tracked_landmarks_list == list(range(103 if appended else 102, 122)) + ([77] if appended else [])

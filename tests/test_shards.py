@@ -160,9 +160,11 @@ class _StubRenderer:
 
 class _StubEngine:
     """Stands in for engine.Engine: each chain appends the true camera centre of the frame it
-    is given, in its own Sim(3) frame; chain 1 of rank 0 fails at its 20th step, and every
-    chain 'fails' when fed the same frame twice (the padding after its shard has ended) --
-    which must not count against it."""
+    is given, in its own Sim(3) frame; the chain of the shard that bootstraps at
+    ``fail_start`` fails at its 20th step, and every chain 'fails' when fed the same frame
+    twice (the padding after its shard has ended) -- which must not count against it."""
+
+    fail_start = 50
 
     def __init__(self, K, opts, W, H, batch, device, ncap, pcap, fcap):
         from types import SimpleNamespace
@@ -179,7 +181,7 @@ class _StubEngine:
 
     def _append(self, b, f):
         k = int(self.t["nF"][b])
-        sc = 0.5 + b + self.rank
+        sc = 0.5 + 0.01 * self.first[b]
         self.t["pose_t"][b, k] = torch.from_numpy(sc * (self.gt[f] - self.gt[self.first[b]]))
         self.t["pose_R"][b, k] = torch.eye(3, dtype=torch.float64).reshape(9)
         self.t["nF"][b] = k + 1
@@ -196,22 +198,23 @@ class _StubEngine:
             f = int(frames[b, 0])
             if self.t["status"][b] != 0:
                 continue
-            if f == self.last[b] or (self.rank == 0 and b == 1 and self.steps == 20):
+            if f == self.last[b] or (self.first[b] == self.fail_start and self.steps == 20):
                 self.t["status"][b] = 1
                 continue
             self._append(b, f)
             self.last[b] = f
 
 
-def _seq_worker(rank, world, port, q):
+def _seq_worker(rank, world, port, q, per_rank=2, groups=None):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RANK"] = str(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from monocular_visual_odometry_va4mr_amd.run_sequence import run
-    res = run("parking", 200, 2, overlap=30, device="cpu", rank=rank, world=world,
-              engine_cls=_StubEngine, renderer=_StubRenderer(), prerender=False)
+    _StubEngine.fail_start = Sh.plan_shards(200, world * per_rank, 2, 30)[1].start
+    res = run("parking", 200, per_rank, overlap=30, device="cpu", rank=rank, world=world,
+              engine_cls=_StubEngine, renderer=_StubRenderer(), prerender=False, groups=groups)
     q.put(None if res is None else {k: v for k, v in res.items() if not k.startswith("_")})
     dist.barrier()
     dist.destroy_process_group()
@@ -239,4 +242,31 @@ def test_run_sequence_bookkeeping_gloo_world2():
     st = rep["stitched"]
     assert st["coverage_breaks"] == [[0, 2, 0]]
     assert [s["shards"] for s in st["segments"]] == [[0], [2, 3]]
+    assert all(s["ate_rel"] < 1e-9 for s in st["segments"])
+
+
+def test_run_sequence_world_x_bseq_plan_gloo_world2():
+    """The sequence job's plan n_shards = world x B_seq (bench.py's sequence leg): 2 ranks x 4
+    shards, each rank's 4 chains split into 2 stream groups (engines).  Shard order, the
+    per-rank blocks and the groups must line up: shard 1 (rank 0, group 0, chain 1) fails and
+    is dropped; shard 2 shares one frame with shard 0 (Parking's bootstrap gap is 6), so it
+    opens a new segment (a reported break); the others stitch exactly (every stand-in chain is
+    a Sim(3) image of the ground truth)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seq_worker, args=(r, 2, port, q, 4, 2)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    rep = [r for r in res if r is not None][0]
+    assert rep["shards"] == 8 and rep["chains_per_gpu"] == 4 and rep["groups"] == 2
+    assert rep["shards_ok"] == 7 and [f["shard"] for f in rep["failed_shards"]] == [1]
+    st = rep["stitched"]
+    assert st["coverage_breaks"] == [[0, 2, 1]]
+    assert [s["shards"] for s in st["segments"]] == [[0], [2, 3, 4, 5, 6, 7]]
     assert all(s["ate_rel"] < 1e-9 for s in st["segments"])

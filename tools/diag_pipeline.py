@@ -4,7 +4,7 @@ import os
 import sys
 import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'tests'))
 sys.path.insert(0, os.path.dirname(HERE))
 from conftest import golden_frames, load_golden  # noqa: E402
 from monocular_visual_odometry_va4mr_amd import options as Op  # noqa: E402

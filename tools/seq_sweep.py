@@ -1,0 +1,56 @@
+"""Sweep of the whole-sequence job (C2, 4541 frames) over the shards per GPU.
+
+    python tools/seq_sweep.py [B ...] [--groups G,G]
+
+For each B: the sequence cut into B shards (30-frame overlap) run as the B chains of one engine
+on this GPU (run_sequence.run), bootstrap timed separately; prints one JSON line per B with
+the wall time, the bootstrap share, the step count and the mean step latency, the unique-frame
+rate 4541 / wall, and the per-shard comparison with the reference fixtures when the cut has one.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run  # noqa: E402
+
+
+def main():
+    argv = sys.argv[1:]
+    Gs = [None]
+    if "--groups" in argv:
+        i = argv.index("--groups")
+        Gs = [int(g) for g in argv[i + 1].split(",")]
+        argv = argv[:i] + argv[i + 2:]
+    Bs = [int(a) for a in argv] or [16, 32, 64, 128, 256]
+    dev = torch.device("cuda", 0)
+    gold = os.path.join(ROOT, "tests", "golden", "kitti_seq00_shards.npz")
+    wide = os.path.join(ROOT, "tests", "golden", "kitti_seq00_shards_wide.npz")
+    for B, G in [(b, g) for b in Bs for g in Gs]:
+        ref = reference_shards(gold, B) or reference_shards(wide, B)
+        best = None
+        for rep in range(3):
+            t0 = time.perf_counter()
+            r = run("kitti", 4541, B, overlap=30, seed=1, device=dev, reference=ref, time_boot=True,
+                    prerender=True, groups=G)
+            tot = time.perf_counter() - t0
+            if best is None or r["wall_s"] < best["wall_s"]:
+                best = r
+            torch.cuda.empty_cache()
+        n_steps = max(s.n_steps for s in best["_plan"])
+        out = {k: v for k, v in best.items() if not k.startswith("_") and k != "stitched"}
+        out["n_steps"] = n_steps
+        out["ms_per_step"] = round(best["step_s"] / n_steps * 1e3, 4)
+        out["call_s"] = round(tot, 2)
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
