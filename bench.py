@@ -79,8 +79,9 @@ def parse():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--no-match", action="store_true", help="skip the C3 / C5 legs (SIFT + BF matcher, C5 step)")
     ap.add_argument("--no-sequence", action="store_true", help="skip the whole-sequence leg")
-    ap.add_argument("--seq-chains", type=int, default=64,
-                    help="shards per GPU of the whole-sequence job (n_shards = world x this)")
+    ap.add_argument("--seq-chains", type=int, default=None,
+                    help="shards per GPU of the whole-sequence job (n_shards = world x this; default "
+                         "seq_chains_for(world))")
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
     return ap.parse_args()
 
@@ -280,6 +281,17 @@ def c5_leg(device, chains=256, steps=6, warmup=2, groups=2):
                               "algorithmic_bytes": gftt_bytes(eng, ncor), "achieved": round(gftt_gbs, 2),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gftt_gbs / HBM_PEAK_GBS, 5)},
             "chains_ok": n_ok}
+
+
+def seq_chains_for(world: int) -> int:
+    """Shards per GPU of the whole-sequence job.  The wall time is bootstrap(B) + (SEQ_LEN /
+    (world B) + 27) x step(B): on one GPU 64 chains minimise it (measured
+    sweep, profiles/r4_seq_sweep.jsonl); with more GPUs each one's shards get shorter, the
+    27-step overlap/bootstrap tail stays, and the step latency falls with B down to the
+    single-chain floor, so B shrinks to keep world x B near 64 (16 per GPU at most 4x over).
+    Reference fixtures exist for every resulting cut (64 shards for 1, 2 and 4 GPUs, 128 for
+    8)."""
+    return max(16, 64 // max(1, world))
 
 
 def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=2):
@@ -533,7 +545,8 @@ def main():
     seq = None
     if not args.no_sequence:
         try:                          # a secondary measurement never costs the headline line
-            seq = sequence_leg(device, args.seed, rank, world, per_gpu=args.seq_chains, groups=args.seq_groups)
+            seq = sequence_leg(device, args.seed, rank, world, per_gpu=args.seq_chains or seq_chains_for(world),
+                               groups=args.seq_groups)
         except Exception as exc:  # noqa: BLE001
             seq = {"error": f"{type(exc).__name__}: {exc}"}
 

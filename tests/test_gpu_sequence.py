@@ -6,9 +6,10 @@ make_long_golden.py: /root/reference/VisualOdometryPipeLine.py on the oracle pri
   bit-identical, so the ATE against the reference trajectory is 0, and where the reference run
   stops with an exception the chain stops at the same frame with the matching status (the
   current fixture: "Not enough keypoints for PnP" at frame 4535, 4533 poses);
-* the sequence cut into 16 and into 8 shards (C4's layout) on the same boundaries as the
-  reference runs: every shard's trajectory bit-identical to its reference run, no failed
-  shard and no coverage break in the stitched trajectory.
+* the sequence cut into 16 and into 8 shards (C4's layout) and into the wider cuts of the
+  sequence job (32 .. 256 shards: shards per GPU as the batch dimension, run in 1 and 2 stream
+  groups) on the same boundaries as the reference runs: every shard's trajectory bit-identical
+  to its reference run, no failed shard and no coverage break in the stitched trajectory.
 
 Frames are rendered on the GPU and checked against the fixture's SHA-1 digests."""
 import hashlib
@@ -83,15 +84,25 @@ def test_full_sequence_matches_reference():
     assert rel == 0.0 or rel < 1e-12
 
 
-@pytest.mark.parametrize("n_shards", [16, 8])
-def test_sharded_sequence_matches_reference_per_shard(n_shards):
+def _shard_fixture(n_shards):
+    for name in ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz"):
+        path = os.path.join(GOLDEN, name)
+        if os.path.exists(path):
+            g = np.load(path, allow_pickle=False)
+            if f"s{n_shards}_t" in g.files:
+                return path, {k: g[k] for k in g.files}
+    pytest.skip(f"no reference fixture for {n_shards} shards (tests/golden/make_long_golden.py --cuts)")
+
+
+@pytest.mark.parametrize("n_shards,groups", [(16, 1), (8, 1), (32, 2), (64, 1), (64, 2), (128, 2), (256, 2)])
+def test_sharded_sequence_matches_reference_per_shard(n_shards, groups):
     from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
-    g = _load("kitti_seq00_shards.npz")
+    path, g = _shard_fixture(n_shards)
     assert all(str(e) == "" for e in g[f"s{n_shards}_error"])
-    ref = reference_shards(os.path.join(GOLDEN, "kitti_seq00_shards.npz"), n_shards)
+    ref = reference_shards(path, n_shards)
     res = run(str(g["preset"]), int(g["n_frames"]), n_shards, overlap=int(g["overlap"]), seed=int(g["seed"]),
-              reference=ref)
-    assert res["shards"] == n_shards
+              reference=ref, groups=groups)
+    assert res["shards"] == n_shards and res["groups"] == groups
     plan = res["_plan"]
     assert np.array_equal(np.array([[s.start, s.boot1, s.end] for s in plan]), g[f"s{n_shards}_bounds"])
     assert res["shards_ok"] == n_shards and res["failed_shards"] == []
