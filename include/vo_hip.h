@@ -240,6 +240,13 @@ int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t
 int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, int64_t img_stride, int W, int H,
                   vo_stream_t stream);
 
+/* Test hook: KeyPointsFilter::retainBest (the SIFT_create(nfeatures) cap, VisualOdometryPipeLine.py:35
+ * with BASELINE C5's nfeatures) as run inside vo_sift_batch, on caller-given rows kp_out [n][6]
+ * (response in column 4), reordered in place; counters[2] = n on entry, the kept count on
+ * return; scratch >= 4 n + 2 ints, tmp >= 6 n floats (all device memory); n <= 32768. */
+int vo_sift_retain_best_rows(float* kp_out, int32_t n, int32_t nfeatures, int32_t* counters, int32_t* scratch,
+                             float* tmp, vo_stream_t stream);
+
 /* BFMatcher().knnMatch(q, t, k=2) (:36,229) for integer-valued float descriptors of
  * dim 128: bf16 MFMA distance tiles (exact), top-2 per query with OpenCV's tie order.
  * nq/nt are read on the device; idx2 [qcap][2] (-1 if absent), dist2 [qcap][2]. */

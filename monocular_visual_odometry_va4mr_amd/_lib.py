@@ -148,6 +148,7 @@ def _declare(L):
         "vo_sift_plan": ([SB, C.c_int, C.c_int], C.c_int),
         "vo_sift": ([SB, P, C.c_int, C.c_int, P], C.c_int),
         "vo_sift_batch": ([SB, C.c_int, P, C.c_int64, C.c_int, C.c_int, P], C.c_int),
+        "vo_sift_retain_best_rows": ([P, i32, i32, P, P, P, P], C.c_int),
         "vo_bf_knn2": ([P, P, P, P, i32, i32, P, P, P], C.c_int),
         "vo_ratio_matches": ([C.c_int, P, P, i32, P, P, P, i32, f64, P, P, P, i32, P], C.c_int),
         "vo_find_essential": ([O, C.c_int, P, P, P, i32, f64, f64, i32, P, P, P, P, i32, P], C.c_int),

@@ -1758,6 +1758,28 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
     return hip_rc();
 }
 
+// Test hook: k_sift_retain_best on caller-given keypoint rows, so its partition
+// rounds can be pinned against libstdc++ on tie-heavy and adversarial response arrays (the
+// SIFT scenes rarely reach them).  counters[2] must hold n on entry and holds the kept count
+// on return; kp_out [n][6] (response in column 4) is reordered in place; scratch >= 4 n + 2
+// ints, tmp >= 6 n floats.
+extern "C" int vo_sift_retain_best_rows(float* kp_out, int32_t n, int32_t nfeatures, int32_t* counters,
+                                        int32_t* scratch, float* tmp, vo_stream_t stream)
+{
+    if (!kp_out || !counters || !scratch || !tmp || n < 0 || n > 32768) return VO_EARG;
+    vo_sift_buf sb;
+    memset(&sb, 0, sizeof sb);
+    sb.counters = counters;
+    sb.cand = scratch;
+    sb.cand_cap = n + 1;                        // 4 cand_cap ints >= 4 n + 2 (rec, LP, RP)
+    sb.kp = tmp;
+    sb.kp_out = kp_out;
+    sb.kp_cap = n;
+    sb.nfeatures = nfeatures;
+    hipLaunchKernelGGL(k_sift_retain_best, dim3(1, 1, 1), dim3(RB_T), 0, (hipStream_t)stream, sb);
+    return hip_rc();
+}
+
 extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream)
 {
     return vo_sift_batch(sb, 1, img, (int64_t)W * H, W, H, stream);

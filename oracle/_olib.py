@@ -56,6 +56,10 @@ def _declare(L):
     L.vo_o_bf_knn2.argtypes = [P, I, P, I, I, P, P]
     L.vo_o_set_fp32_mode.argtypes = [I]
     L.vo_o_set_fp32_mode.restype = None
+    L.vo_o_set_svd_form.argtypes = [I]
+    L.vo_o_set_svd_form.restype = None
+    L.vo_o_get_svd_form.argtypes = []
+    L.vo_o_get_svd_form.restype = I
     L.vo_o_rng_next.argtypes = [P]
     L.vo_o_rng_next.restype = C.c_uint32
 
@@ -64,6 +68,17 @@ def set_fp32_mode(mode: int) -> None:
     """0: integer-exact GFTT / LK sums (the parity oracle); bit 0: OpenCV-style fp32
     cornerMinEigenVal; bit 1: LK sums in float (measurement only, see vo_oracle_img.c)."""
     lib().vo_o_set_fp32_mode(int(mode))
+
+
+def set_svd_form(form: int) -> None:
+    """EPnP's 12x12 SVD of M^T M: 0 = QUARTER_SUM partial sums + u / wn rotation (the GPU's order;
+    every golden fixture assumes it), 1 = the round-2 serial sums + t / c / s rotation (an
+    independent cross-check, never the parity oracle)."""
+    lib().vo_o_set_svd_form(int(form))
+
+
+def get_svd_form() -> int:
+    return int(lib().vo_o_get_svd_form())
 
 
 def ptr(a: np.ndarray | None):

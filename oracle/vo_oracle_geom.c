@@ -119,8 +119,24 @@ static void svd_jacobi(double* A, int m, int n, double* w, double* V)
  * Stopping rule, sort and normalisation as svd_jacobi.  (OpenCV's JacobiSVD uses the cyclic
  * order and its own summation; the decompositions agree to rounding -- OpenCV-level parity is
  * unpinned anyway, and the GPU follows this order exactly.) */
+/* The round-2 form of svd_jacobi_rr -- serial column sums k = 0..m-1 and the rotation as
+ * t = sign / u, c = 1 / sqrt(1 + t^2), s = c t -- kept as an independent cross-check of the
+ * round-3 form (QUARTER_SUM + u / wn) that the GPU follows and every golden assumes
+ * (vo_o_set_svd_form(1); tests/test_oracle_kat.py, tools/svd_form_trajectory.py). */
+static int g_svd_form = 0;
+void vo_o_set_svd_form(int form) { g_svd_form = form; }
+int vo_o_get_svd_form(void) { return g_svd_form; }
+
+#define SERIAL_SUM(res, m, expr)                                               \
+    do {                                                                       \
+        double ss_ = 0;                                                        \
+        for (int k = 0; k < (m); ++k) ss_ += (expr);                           \
+        (res) = ss_;                                                           \
+    } while (0)
+
 static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
 {
+    const int serial = g_svd_form == 1;
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
@@ -131,17 +147,31 @@ static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
                 const int b = ((n - 2 - q + r) % (n - 1)) + 1;
                 const int i = a < b ? a : b, j = a < b ? b : a;
                 double alpha, beta, gamma;
-                QUARTER_SUM(alpha, m, A[k * n + i] * A[k * n + i]);
-                QUARTER_SUM(beta, m, A[k * n + j] * A[k * n + j]);
-                QUARTER_SUM(gamma, m, A[k * n + i] * A[k * n + j]);
+                if (serial) {
+                    SERIAL_SUM(alpha, m, A[k * n + i] * A[k * n + i]);
+                    SERIAL_SUM(beta, m, A[k * n + j] * A[k * n + j]);
+                    SERIAL_SUM(gamma, m, A[k * n + i] * A[k * n + j]);
+                } else {
+                    QUARTER_SUM(alpha, m, A[k * n + i] * A[k * n + i]);
+                    QUARTER_SUM(beta, m, A[k * n + j] * A[k * n + j]);
+                    QUARTER_SUM(gamma, m, A[k * n + i] * A[k * n + j]);
+                }
                 if (alpha == 0.0 || beta == 0.0) continue;
                 if (fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
                 changed = 1;
                 const double zeta = (beta - alpha) / (2.0 * gamma);
-                const double u = fabs(zeta) + sqrt(1.0 + zeta * zeta);
-                const double wn = sqrt(u * u + 1.0);
-                const double c = u / wn;
-                const double s = (zeta < 0 ? -1.0 : 1.0) / wn;
+                double c, s;
+                if (serial) {
+                    double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    if (zeta < 0) t = -t;
+                    c = 1.0 / sqrt(1.0 + t * t);
+                    s = c * t;
+                } else {
+                    const double u = fabs(zeta) + sqrt(1.0 + zeta * zeta);
+                    const double wn = sqrt(u * u + 1.0);
+                    c = u / wn;
+                    s = (zeta < 0 ? -1.0 : 1.0) / wn;
+                }
                 for (int k = 0; k < m; ++k) {
                     double ai = A[k * n + i], aj = A[k * n + j];
                     A[k * n + i] = c * ai - s * aj;
@@ -158,7 +188,8 @@ static void svd_jacobi_rr(double* A, int m, int n, double* w, double* V)
     }
     for (int i = 0; i < n; ++i) {
         double s;
-        QUARTER_SUM(s, m, A[k * n + i] * A[k * n + i]);
+        if (serial) SERIAL_SUM(s, m, A[k * n + i] * A[k * n + i]);
+        else QUARTER_SUM(s, m, A[k * n + i] * A[k * n + i]);
         w[i] = sqrt(s);
     }
     for (int i = 0; i < n - 1; ++i) {

@@ -246,8 +246,13 @@ def test_batched_bootstrap_matches_oracle_per_chain():
     opts, _, _ = Op.get("kitti")
     starts = [0, 2, 4, 6, 8, 11]
     eng = Engine(K, opts, 1241, 376, batch=len(starts), ncap=4096, pcap=8192, fcap=16)
-    eng.bootstrap(fr[starts], fr[[s + 2 for s in starts]], sift_batch_bytes=4 * Sift.bytes_per_image(1241, 376))
-    assert eng._sift.batch == 4
+    budget = 4 * Sift.bytes_per_image(1241, 376)
+    sift, m = eng.reserve_bootstrap(budget)          # reserved by the caller: kept after bootstrap
+    assert sift.batch == 4 and m == 2
+    eng.bootstrap(fr[starts], fr[[s + 2 for s in starts]], sift_batch_bytes=budget)
+    assert eng._sift is sift
+    eng.release_bootstrap()
+    assert eng._sift is None
     for b, s0 in enumerate(starts):
         s = V.new_state(K, opts)
         V.initialize(s, fr[s0], fr[s0 + 2])
@@ -259,3 +264,62 @@ def test_batched_bootstrap_matches_oracle_per_chain():
         for name, ref in (("landmarks", s.lm), ("keypoints", s.kp), ("cand", s.cand),
                           ("cand_first", s.cand_first), ("cand_tau", s.cand_tau)):
             assert np.array_equal(e[name], ref), f"chain {b} {name}"
+
+
+def test_bootstrap_sift_capacity_marks_only_the_overflowing_chain(monkeypatch):
+    """a chain whose SIFT keypoints exceed the capacity gets VO_ST_CAPACITY on the
+    device (no host check inside bootstrap); the other chains of the batch are unaffected --
+    bootstrap pose and state identical to an uncapped run, and they step on identically while
+    the failed chain is skipped (its pose count stays); the drop-in class raises after
+    initialization on such a pair."""
+    from monocular_visual_odometry_va4mr_amd import _lib as L
+    from monocular_visual_odometry_va4mr_amd import features as F
+    from monocular_visual_odometry_va4mr_amd import options as Op
+    from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    from monocular_visual_odometry_va4mr_amd.VisualOdometryPipeLine import VisualOdometryPipeLine
+    fr, K, _, _ = make_sequence("kitti", 14, seed=1)
+    opts, _, _ = Op.get("kitti")
+    starts = [0, 3, 6, 9]
+    f0, f1 = fr[starts], fr[[s + 2 for s in starts]]
+
+    def run(cap=None):
+        if cap is not None:
+            monkeypatch.setattr(F, "default_kp_cap", lambda w, h: cap)
+        eng = Engine(K, opts, 1241, 376, batch=len(starts), ncap=8192, pcap=8192, fcap=16)
+        sift, m = eng.reserve_bootstrap()
+        assert m == len(starts)                       # one chunk: image rows b and B + b
+        eng.bootstrap(f0, f1)
+        torch.cuda.synchronize()
+        raw = sift.t["counters"][:2 * len(starts), 1].cpu().numpy()     # appended before dedup
+        n = np.maximum(raw[:len(starts)], raw[len(starts):])
+        eng.release_bootstrap()
+        for j in (3, 4):
+            eng.step(fr[[s + j for s in starts]])
+        torch.cuda.synchronize()
+        monkeypatch.undo()
+        return eng, n
+
+    ref, n = run()
+    assert (ref.statuses() == 0).all()
+    order = np.argsort(n)
+    assert n[order[-1]] > n[order[-2]], "needs one chain with the largest keypoint count"
+    bad = int(order[-1])
+    eng, _ = run(cap=int(n[order[-2]]) + 1)            # every other chain fits exactly
+    st = eng.statuses()
+    assert st[bad] == L.ST_CAPACITY and all(st[b] == 0 for b in range(len(starts)) if b != bad)
+    assert int(eng.t["nF"][bad]) == 2                 # skipped by both steps
+    for b in range(len(starts)):
+        if b == bad:
+            continue
+        e, r = eng.export_chain(b), ref.export_chain(b)
+        assert len(e["transforms"]) == len(r["transforms"]) == 4
+        for (Re, te), (Rr, tr) in zip(e["transforms"], r["transforms"]):
+            assert np.array_equal(Re, Rr) and np.array_equal(te, tr)
+        for k in ("landmarks", "keypoints", "cand", "cand_first", "cand_tau"):
+            assert np.array_equal(e[k], r[k]), (b, k)
+    # the drop-in class on the overflowing pair: initialization raises (chain status)
+    monkeypatch.setattr(F, "default_kp_cap", lambda w, h: int(n[order[-2]]) + 1)
+    vo = VisualOdometryPipeLine(K, opts, max_frames=16, landmark_capacity=8192, candidate_capacity=8192)
+    with pytest.raises(RuntimeError, match="capacity"):
+        vo.initialization(f0[bad], f1[bad])

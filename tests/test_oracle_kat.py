@@ -57,6 +57,34 @@ def test_p3p_epnp_exact(scene):
     assert ok and np.abs(Re - R).max() < 1e-10 and np.abs(te - t).max() < 1e-9
 
 
+def test_epnp_svd_forms_agree():
+    """EPnP's 12x12 SVD follows the GPU's order (QUARTER_SUM sums, u / wn rotation),
+    which every golden assumes; the round-2 serial form stays in the oracle as an independent
+    cross-check.  On noisy, outlier-free problems (pixel noise 0.5, 8..400 points) both forms
+    give the same pose to rounding: |dR| <= 1e-9, |dt| <= 1e-9 x (1 + |t|)."""
+    assert O.get_svd_form() == 0, "the parity oracle must run the GPU's SVD form"
+    rng = np.random.default_rng(11)
+    try:
+        for trial in range(60):
+            n = int(rng.integers(8, 400))
+            R = _rot(rng.normal(size=3), rng.uniform(0, 0.6))
+            t = rng.normal(size=3) * [1, 0.3, 2]
+            X = rng.uniform([-8, -3, 6], [8, 3, 60], (n, 3))
+            Xc = X @ R.T + t
+            x = Xc @ K.T
+            x = x[:, :2] / x[:, 2:] + rng.normal(scale=0.5, size=(n, 2))
+            O.set_svd_form(0)
+            ok0, R0, t0 = O.epnp(K, X, x)
+            O.set_svd_form(1)
+            ok1, R1, t1 = O.epnp(K, X, x)
+            assert ok0 and ok1
+            dr = np.abs(R0 - R1).max()
+            dt = np.abs(t0 - t1).max() / (1 + np.abs(t0).max())
+            assert dr <= 1e-9 and dt <= 1e-9, (trial, dr, dt)
+    finally:
+        O.set_svd_form(0)
+
+
 def test_pnp_ransac_with_outliers(scene):
     R, t, X, x = scene
     x2 = x.copy()
