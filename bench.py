@@ -83,6 +83,8 @@ def parse():
                     help="shards per GPU of the whole-sequence job (n_shards = world x this; default "
                          "seq_chains_for(world))")
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; <= 32)")
     return ap.parse_args()
 
 
@@ -427,6 +429,8 @@ def gpu_chain_positions(K, opts, frames_dev, device):
 
 def main():
     args = parse()
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -787,7 +787,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const int ish = gx & 3;
                 const int ln = lane + opaque0();
                 const int vi = loff + gy * pitch + (gx & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);   // 8 dwords / row
-                const int vd = 4 * (loff + gy * pitch + gx + (ln >> 4) * pitch + (ln & 15));    // 16 (dx, dy) / row
+                // 16 (dx, dy) per row; lane -> row 4k + 2 ((ln >> 4) & 1) + (ln >> 5): the two rows a
+                // 32-lane half stores are 2 apart (2 QS = 48 dwords, 16 banks), so the ds_write_b32
+                // of DR below is conflict-free (rows r, r + 1 at QS = 24 collided 2-way)
+                const int drow = 2 * ((ln >> 4) & 1) + (ln >> 5);
+                const int vd = 4 * (loff + gy * pitch + gx + drow * pitch + (ln & 15));
                 uint32_t vir[NIR], vdd[NDR], vjr[NJR];
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
@@ -816,7 +820,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 }
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
-                    const int r = (ln >> 4) + 4 * k, c = ln & 15;
+                    const int r = drow + 4 * k, c = ln & 15;
                     DR[r * QS + c] = vdd[k];
                 }
                 if (staged) j_store(vjr);      // syncs
@@ -855,10 +859,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     iseed[j] = 256u - ((uint32_t)ival[j] << 9);
                     ixv[j] = live[j] ? gx2 : 0;
                     iyv[j] = live[j] ? gy2 : 0;
-                    a11 += __mul24(ixv[j], ixv[j]);
-                    a12 += __mul24(ixv[j], iyv[j]);
-                    a22 += __mul24(iyv[j], iyv[j]);
                 }
+                // the gradients as int16 pairs of pixels (0, 1) and (2, 3) (|dI| <= 4080): the
+                // tensor here and the iteration's b1, b2 below are v_dot2_i32_i16 sums (exact)
+                const v2i16 gxp0 = as_v2i16(__builtin_amdgcn_perm((uint32_t)ixv[1], (uint32_t)ixv[0], 0x05040100u));
+                const v2i16 gxp1 = as_v2i16(__builtin_amdgcn_perm((uint32_t)ixv[3], (uint32_t)ixv[2], 0x05040100u));
+                const v2i16 gyp0 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[1], (uint32_t)iyv[0], 0x05040100u));
+                const v2i16 gyp1 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[3], (uint32_t)iyv[2], 0x05040100u));
+                a11 = __builtin_amdgcn_sdot2(gxp0, gxp0, __builtin_amdgcn_sdot2(gxp1, gxp1, 0, false), false);
+                a12 = __builtin_amdgcn_sdot2(gxp0, gyp0, __builtin_amdgcn_sdot2(gxp1, gyp1, 0, false), false);
+                a22 = __builtin_amdgcn_sdot2(gyp0, gyp0, __builtin_amdgcn_sdot2(gyp1, gyp1, 0, false), false);
                 // one exact 32-bit reduction each unless a lane's partial could overflow the sum
                 const bool twide = __ballot((uint32_t)a11 >= (1u << 25) || (uint32_t)a22 >= (1u << 25) ||
                                             (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
@@ -920,16 +930,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     for (int j = 0; j < MAXJ; ++j) qv[j] = tb[toff[j]];
                     // the iw11 = -1 correction only in its own (wave-uniform) copy of the loop
                     auto mismatch = [&](auto negc) {
+                        uint32_t dd[MAXJ];
 #pragma unroll
                         for (int j = 0; j < MAXJ; ++j) {
                             const uint32_t q = qv[j];
                             uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
                                            __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                             if (decltype(negc)::value) sum -= q >> 24;
-                            const int diff = (int)sum >> 9;
-                            b1 += __mul24(diff, ixv[j]);      // |diff| <= 8160, |grad| <= 4080
-                            b2 += __mul24(diff, iyv[j]);
+                            dd[j] = (uint32_t)((int)sum >> 9);       // |diff| <= 8160: an int16
                         }
+                        // b1 = sum diff * Ix, b2 = sum diff * Iy as int16-pair dot products
+                        const v2i16 d01 = as_v2i16(__builtin_amdgcn_perm(dd[1], dd[0], 0x05040100u));
+                        const v2i16 d23 = as_v2i16(__builtin_amdgcn_perm(dd[3], dd[2], 0x05040100u));
+                        b1 = __builtin_amdgcn_sdot2(d01, gxp0, __builtin_amdgcn_sdot2(d23, gxp1, 0, false), false);
+                        b2 = __builtin_amdgcn_sdot2(d01, gyp0, __builtin_amdgcn_sdot2(d23, gyp1, 0, false), false);
                     };
                     if (neg) mismatch(std::true_type());
                     else mismatch(std::false_type());

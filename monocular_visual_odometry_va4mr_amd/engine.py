@@ -261,8 +261,21 @@ class Engine:
             # process that had made other streams: 0.75 instead of 0.50 ms per frame).  For
             # small batches the side stream comes from the high-priority pool, whose queues are
             # never those of a normal-priority main stream.
-            self._side = torch.cuda.Stream(self.device, priority=-1 if self.B <= 16 else 0)
+            hi = self.B <= 16 or self._prio_latency()
+            self._side = torch.cuda.Stream(self.device, priority=-1 if hi else 0)
         return self._side
+
+    @staticmethod
+    def _prio_latency() -> bool:
+        return os.environ.get("VO_PRIO_LATENCY") == "1"
+
+    def _latency_stream(self):
+        """VO_PRIO_LATENCY=1: the one-block-per-chain stages (PnP + triangulation, the step
+        finish) on a high-priority stream of their own, so that the dispatcher hands them CUs
+        before the queued tracking blocks of another stream group (measurement option)."""
+        if getattr(self, "_lat", None) is None:
+            self._lat = torch.cuda.Stream(self.device, priority=-1)
+        return self._lat
 
     def _step_launch(self, frames, prev, marks=None, gftt_late=False):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
@@ -299,16 +312,23 @@ class Engine:
         run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
         if gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
+        lat = main
+        if self._prio_latency() and forked:
+            lat = self._latency_stream()
+            lat.wait_stream(main)                                 # tracking done
+        sl = C.c_void_p(lat.cuda_stream)
         if getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1"):
             # one launch for both stages (vo_pnp_triangulate); stage 3 is then empty
-            run(2, main, lambda: lib.vo_pnp_triangulate(pd, po, ps, sm))
-            run(3, main, lambda: 0)
+            run(2, lat, lambda: lib.vo_pnp_triangulate(pd, po, ps, sl))
+            run(3, lat, lambda: 0)
         else:
-            run(2, main, lambda: lib.vo_pnp(pd, po, ps, sm))
-            run(3, main, lambda: lib.vo_triangulate(pd, po, ps, 0, sm))
+            run(2, lat, lambda: lib.vo_pnp(pd, po, ps, sl))
+            run(3, lat, lambda: lib.vo_triangulate(pd, po, ps, 0, sl))
         if forked:
-            main.wait_stream(side)                                # corners ready
-        run(5, main, lambda: lib.vo_add_corners_finish(pd, po, ps, sm))
+            lat.wait_stream(side)                                 # corners ready
+        run(5, lat, lambda: lib.vo_add_corners_finish(pd, po, ps, sl))
+        if lat is not main:
+            main.wait_stream(lat)                                 # the step ends on main
 
     def capture_step(self):
         """Capture the two ping-pong variants of the step into hipGraphs; returns a
