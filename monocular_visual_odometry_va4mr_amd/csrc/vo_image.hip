@@ -604,8 +604,9 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // 15x15 for every dataset, main.py:36,66,96), with all window data staged through LDS by
 // coalesced dword loads instead of per-lane byte gathers:
 //   IR/DR  raw rows of I (u8) and dI (int16 pairs) under the (WW+1)x(WH+1) bilinear window,
-//   JR     raw rows of J under the (TW+1)x(TH+1) tile, TW = WW + 2M,
-//   QT     the J tile as packed 2x2 quads (built from JR), read by the iterations.
+//   QT     the J tile ((TW+1)x(TH+1), TW = WW + 2M) as packed 2x2 quads, read by the
+//          iterations; built straight from registers (rows r and r + 1 loaded by every lane,
+//          the next dword from the neighbouring lane): no raw-row LDS image.
 // The tile origin is clamped so every staged row lies inside the padded level; dword rows
 // may run up to 3 bytes past a row end (next row, or the >= 64-byte tail slack that the
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
@@ -619,20 +620,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     constexpr int JRW = (TW + 1 + 3 + 3) / 4, IRW = (WW + 1 + 3 + 3) / 4, DRW = WW + 1;
     constexpr int QM = (TW + 3) / 4, QS = 4 * QM;      // QT: quads of 4 columns, row stride QS
     // LDS rows: QT quads, the I window bytes and the dI dwords all have the row stride QS (in
-    // their element), so one per-lane offset toff = row * QS + col indexes all three; JR rows
-    // are 8 dwords, so the staging lane -> (row, dword) map is (lane / 8, lane % 8)
+    // their element), so one per-lane offset toff = row * QS + col indexes all three; J rows are
+    // loaded as 8 dwords, so the staging lane -> (row, dword) map is (lane / 8, lane % 8)
     constexpr int IRS = QS / 4, JRS = 8;
     static_assert(JRW >= QM + 1 && JRW <= JRS && IRW <= IRS && IRW <= 8 && DRW == 16 && QS % 4 == 0,
                   "k_lk_w staging layout");
     // one spare row in QT / IR / DR: read (never used) by the dead lanes of window row 15
     __shared__ uint4 QT4_all[WPB][(TH + 1) * QM];
-    __shared__ uint32_t JR_all[WPB][(TH + 1) * JRS];
     __shared__ uint32_t IR_all[WPB][(WH + 2) * IRS];
     __shared__ uint32_t DR_all[WPB][(WH + 2) * QS];
     const int wv = WPB > 1 ? (int)(threadIdx.x >> 6) : 0;
     uint4* QT4 = QT4_all[wv];
     const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
-    uint32_t* JR = JR_all[wv];
     uint32_t* IR = IR_all[wv];
     uint32_t* DR = DR_all[wv];
     const uint8_t* ir8 = (const uint8_t*)IR;
@@ -677,52 +676,58 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     // and store (LDS writes), so that every load of a stage is in flight at once: one memory
     // round trip per stage instead of one per loop trip.
     constexpr int NIR = ((WH + 1) * 8 + 63) / 64, NDR = ((WH + 1) * 16 + 63) / 64;
-    constexpr int NJR = ((TH + 1) * JRS + 63) / 64, NQT = (TH * QM + 63) / 64;
+    constexpr int NJR = (TH * JRS + 63) / 64;             // 8 quad rows per load round
     // J tile origin covering the window at (inx, iny)
     auto j_origin = [&](int inx, int iny) {
         tx0 = max(inx - LK_M, -VO_BORDER);
         ty0 = min(max(iny - LK_M, -VO_BORDER), rows + VO_BORDER - 1 - TH);
         jsh = (tx0 + VO_BORDER) & 3;
     };
-    auto j_issue = [&](uint32_t (&v)[NJR]) {
+    // J rows r (a) and r + 1 (b) of the tile straight into registers, lane -> row 8 k + lane / 8
+    // (+ 1 for b), aligned dword lane % 8 -- no raw-row LDS image: the quad build below takes
+    // the dword to the right from the neighbouring lane (DPP) and row r + 1 from its own b load
+    auto j_issue = [&](uint32_t (&v)[2][NJR]) {
         const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
         const int ln = lane + opaque0();
         const int vo = loff + gy0 * pitch + (gx0 & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
-            v[k] = 0u;
-            if ((lane >> 3) + 8 * k < TH + 1) {
-                LKCHKO(vo + 8 * k * pitch, P.pstride, "J");
-                v[k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, vo, 8 * k * pitch, 0);
+            v[0][k] = 0u;
+            v[1][k] = 0u;
+            if ((lane >> 3) + 8 * k < TH) {               // quad rows 0 .. TH - 1 use rows r, r + 1
+                LKCHKO(vo + 8 * k * pitch + pitch, P.pstride, "J");
+                v[0][k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, vo, 8 * k * pitch, 0);
+                v[1][k] = __builtin_amdgcn_raw_buffer_load_b32(rJ, vo, 8 * k * pitch + pitch, 0);
             }
         }
     };
-    // JR rows -> LDS, then the packed 2x2 quads QT: one item = row r, columns 4m..4m+3, built
-    // from four aligned JR dwords with byte-align and two rounds of byte permutes and stored as
-    // one 16-B write; quad byte order (J[r][c], J[r][c+1], J[r+1][c], J[r+1][c+1])
-    auto j_store = [&](const uint32_t (&v)[NJR]) {
+    // the packed 2x2 quads QT: one item = quad row r, columns 4m..4m+3 (lane: r = 8 k + lane / 8,
+    // m = lane % 8 < QM), built from the aligned dwords m, m + 1 of rows r and r + 1 (dword m + 1
+    // from lane + 1 by DPP row_shl:1; m + 1 <= QM < 8 stays in the lane's 8-group) with byte-align
+    // and two rounds of byte permutes, stored as one 16-B write; quad byte order (J[r][c],
+    // J[r][c+1], J[r+1][c], J[r+1][c+1])
+    auto j_store = [&](const uint32_t (&v)[2][NJR]) {
+        const int ln = lane + opaque0();
+        const int m = ln & 7;
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
-            const int q = lane + 64 * k;
-            if (q < (TH + 1) * JRS) JR[q] = v[k];
-        }
-        wave_lds_sync();
-        const int ln = lane + opaque0();
-#pragma unroll
-        for (int k = 0; k < NQT; ++k) {
-            const int q = ln + 64 * k;
-            if (q < TH * QM) {
-                const int r = q / QM, m = q - r * QM;
-                const uint32_t* j0 = JR + r * JRS + m;
-                const uint32_t a0 = j0[0], a1 = j0[1], b0 = j0[JRS], b1 = j0[JRS + 1];
+            const uint32_t a0 = v[0][k], b0 = v[1][k];
+            const uint32_t a1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a0, 0x101, 0xF, 0xF, false);   // row_shl:1
+            const uint32_t b1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b0, 0x101, 0xF, 0xF, false);
+            const int r = (ln >> 3) + 8 * k;
+#ifdef VO_LKX_NOQT
+            if (false) {
+#else
+            if (m < QM && r < TH) {
+#endif
                 const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
                 const uint32_t Bv = jsh == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, jsh + 1);
                 const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
                 const uint32_t D = jsh == 3 ? b1 : __builtin_amdgcn_alignbyte(b1, b0, jsh + 1);
                 const uint32_t X = __builtin_amdgcn_perm(Bv, A, 0x05010400u), Y = __builtin_amdgcn_perm(Bv, A, 0x07030602u);
                 const uint32_t Xp = __builtin_amdgcn_perm(D, C, 0x05010400u), Yp = __builtin_amdgcn_perm(D, C, 0x07030602u);
-                QT4[q] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
-                                    __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
+                QT4[r * QM + m] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
+                                             __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
             }
         }
         wave_lds_sync();
@@ -732,7 +737,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
         LKPROF_ADD(3, 1);
         LKPROF_T(tj0);
         j_origin(inx, iny);
-        uint32_t v[NJR];
+        uint32_t v[2][NJR];
         j_issue(v);
         wave_lds_sync();
         j_store(v);
@@ -792,16 +797,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // of DR below is conflict-free (rows r, r + 1 at QS = 24 collided 2-way)
                 const int drow = 2 * ((ln >> 4) & 1) + (ln >> 5);
                 const int vd = 4 * (loff + gy * pitch + gx + drow * pitch + (ln & 15));
-                uint32_t vir[NIR], vdd[NDR], vjr[NJR];
+                uint32_t vir[NIR], vdd[NDR], vjr[2][NJR];
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
                     LKCHKO(vi + 8 * k * pitch, P.pstride, "I");
+#ifdef VO_LKX_NOSTAGE
+                    vir[k] = (uint32_t)(vi + k) * 0x01010101u;
+#else
                     vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, vi, 8 * k * pitch, 0);
+#endif
                 }
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
                     LKCHKO(vd + 16 * k * pitch, 2 * P.dstride, "D");
+#ifdef VO_LKX_NOSTAGE
+                    vdd[k] = (uint32_t)(vd * 7 + k) & 0x00ff00ffu;
+#else
                     vdd[k] = __builtin_amdgcn_raw_buffer_load_b32(rD, vd, 16 * k * pitch, 0);
+#endif
                 }
                 {
                     const int jx = (int)floorf(ox - hx), jy = (int)floorf(oy - hy);
@@ -844,11 +857,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
+#ifdef VO_LKX_NOTENSOR
+                    const uint32_t d00 = (uint32_t)(toff[j] * 977) & 0x03ff03ffu, d01 = d00 + 3, d10 = d00 + 5, d11 = d00 + 9;
+                    const int v = (toff[j] * 31) & 8191;
+#else
                     const uint8_t* s = ir8 + toff[j] + ish;
                     const uint32_t* d = DR + toff[j];
                     const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
                     const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
                                           __mul24((int)s[QS], iw10) + __mul24((int)s[QS + 1], iw11), 9);
+#endif
                     const int gx2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x05040100u)), wp1,
                                         __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x05040100u)), wp0,
                                                                1 << 13, false), false) >> 14;
@@ -978,7 +996,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     LKPROF_T(te);
                     LKPROF_ADD(7, te - ta1);
                 }
+#ifdef VO_LKX_NOERR
+                if (false) {
+#else
                 if (status && level == 0) {
+#endif
                     const float fx = ox - hx, fy = oy - hy;
                     const int inx = (int)floorf(fx), iny = (int)floorf(fy);
                     if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {

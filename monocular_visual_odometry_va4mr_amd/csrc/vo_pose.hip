@@ -1160,8 +1160,11 @@ extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_s
     fill_tri(T, d, o, s, 0);
     // more chains than CUs: the 2-waves/SIMD build (two blocks per CU, some registers spilled);
     // otherwise every block has a CU of its own and the unconstrained build is faster
+    // (VO_PNP_TRI_WPE=1|2 forces one build: measurement option)
+    static const int force = [] { const char* e = getenv("VO_PNP_TRI_WPE"); return e ? atoi(e) : 0; }();
     const int n_cu = device_cus() > 0 ? device_cus() : 256;      // of the current device
-    if (d->B > n_cu) hipLaunchKernelGGL(k_pnp_tri<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
+    const bool two = force ? force == 2 : d->B > n_cu;
+    if (two) hipLaunchKernelGGL(k_pnp_tri<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     else hipLaunchKernelGGL(k_pnp_tri<1>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     return hip_rc();
 }

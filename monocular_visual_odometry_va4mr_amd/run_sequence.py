@@ -109,6 +109,12 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
             b = min(hi, a + 32)
             cache[a - lo:b - lo] = renderer.render_batch(list(range(a, b)), Rs[a:b], cs[a:b])
         idx_dev = torch.from_numpy(idx - lo).to(dev)
+        # every step's frames laid out once as [n_steps][B] (rows of a group contiguous), so a
+        # step reads its frames in place: no gather kernel on the critical path of each step
+        # (~40 us per group-step at 32 KITTI chains); ~0.47 MB per chain-step
+        steps = torch.empty((n_steps, B, renderer.H, renderer.W), dtype=torch.uint8, device=dev)
+        for j in range(n_steps):
+            torch.index_select(cache, 0, idx_dev[j], out=steps[j])
 
     def frames_at(ids):
         ids = [min(int(i), n_frames - 1) for i in ids]
@@ -118,7 +124,7 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
 
     def step_frames(j, g):
         if idx_dev is not None:
-            return cache.index_select(0, idx_dev[j, bounds[g]:bounds[g + 1]])
+            return steps[j, bounds[g]:bounds[g + 1]]
         return frames_at(idx[j, bounds[g]:bounds[g + 1]])
 
     def on(g):

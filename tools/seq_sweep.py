@@ -25,6 +25,11 @@ from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, r
 def main():
     argv = sys.argv[1:]
     Gs = [None]
+    reps = 3
+    if "--reps" in argv:
+        i = argv.index("--reps")
+        reps = int(argv[i + 1])
+        argv = argv[:i] + argv[i + 2:]
     if "--groups" in argv:
         i = argv.index("--groups")
         Gs = [int(g) for g in argv[i + 1].split(",")]
@@ -36,7 +41,7 @@ def main():
     for B, G in [(b, g) for b in Bs for g in Gs]:
         ref = reference_shards(gold, B) or reference_shards(wide, B)
         best = None
-        for rep in range(3):
+        for rep in range(reps):
             t0 = time.perf_counter()
             r = run("kitti", 4541, B, overlap=30, seed=1, device=dev, reference=ref, time_boot=True,
                     prerender=True, groups=G)
