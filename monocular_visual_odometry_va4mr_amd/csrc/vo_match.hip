@@ -233,10 +233,26 @@ __global__ void __launch_bounds__(256) k_bf_mfma(BfArgs A)
 //                largest s with ties to the lowest train index of the lane; the sub-tile's two
 //                largest keys come from four v_max / v_med3 running top-2 chains merged pairwise,
 //                and only they are tested against the lane's running second-best.
-__global__ void __launch_bounds__(256) k_bf_prep_i8(const float* __restrict__ src, const int32_t* n, int B, int cap,
-                                                    int8_t* __restrict__ dst, int32_t* __restrict__ nrm)
+// Both operands in one launch: blocks [0, qblocks) prepare the queries, the rest the train rows;
+// block 0 also clears the fixup-list counter (the merge appends to it later in stream order).
+struct BfPrep {
+    const float* src;
+    const int32_t* n;
+    int cap;
+    int8_t* dst;
+    int32_t* nrm;
+};
+__global__ void __launch_bounds__(256) k_bf_prep_i8(BfPrep Q, BfPrep T, int B, int qblocks, int32_t* flag_n)
 {
-    const int row = blockIdx.x * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+    const bool isq = (int)blockIdx.x < qblocks;
+    const BfPrep& X = isq ? Q : T;
+    const float* __restrict__ src = X.src;
+    const int32_t* n = X.n;
+    const int cap = X.cap;
+    int8_t* __restrict__ dst = X.dst;
+    int32_t* __restrict__ nrm = X.nrm;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag_n = 0;
+    const int row = ((int)blockIdx.x - (isq ? 0 : qblocks)) * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
     const int b = row / cap, r = row - b * cap;
     const bool ok = b < B && r < n[min(b, B - 1)];
     int ss = 0;
@@ -446,7 +462,14 @@ __global__ void __launch_bounds__(256) k_bf_merge(BfArgs A)
 {
     const int row = blockIdx.x * blockDim.x + threadIdx.x;
     const int b = row / A.qcap, q = row - b * A.qcap;
-    if (b >= A.B || q >= A.nq[b]) return;
+    if (b >= A.B) return;
+    if (q >= A.nq[b]) {                      // no query: the absent pair (-1, FLT_MAX) x 2
+        int32_t* ix = A.idx2 + ((int64_t)b * A.qcap + q) * 2;
+        float* ds = A.dist2 + ((int64_t)b * A.qcap + q) * 2;
+        ix[0] = ix[1] = -1;
+        ds[0] = ds[1] = FLT_MAX;
+        return;
+    }
     int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
     const int per = bf_per(A.nt[b], A);
     for (int sp = 0; sp < A.tsplit; ++sp) {
@@ -562,15 +585,14 @@ extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_
     A.flag_n = (int32_t*)p; p += 256;
     A.flag_list = (int32_t*)p;
     A.nq = nq; A.nt = nt; A.idx2 = idx2; A.dist2 = dist2;
-    if (hipMemsetAsync(A.flag_n, 0, sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
     const int nqb = (qcap + A.qb - 1) / A.qb;
     if (!use_bf16) {
-        hipLaunchKernelGGL(k_bf_prep_i8, dim3(((int64_t)B * qcap + 31) / 32), dim3(256), 0, st, q, nq, B, qcap,
-                           (int8_t*)A.qbf, (int32_t*)A.qn);
-        hipLaunchKernelGGL(k_bf_prep_i8, dim3(((int64_t)B * tcap + 31) / 32), dim3(256), 0, st, t, nt, B, tcap,
-                           (int8_t*)A.tbf, (int32_t*)A.tn);
+        const int qblocks = (int)(((int64_t)B * qcap + 31) / 32), tblocks = (int)(((int64_t)B * tcap + 31) / 32);
+        const BfPrep Q{q, nq, qcap, (int8_t*)A.qbf, (int32_t*)A.qn}, T{t, nt, tcap, (int8_t*)A.tbf, (int32_t*)A.tn};
+        hipLaunchKernelGGL(k_bf_prep_i8, dim3(qblocks + tblocks), dim3(256), 0, st, Q, T, B, qblocks, A.flag_n);
         hipLaunchKernelGGL((k_bf_i8<BFI_TT, 1>), dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
     } else {
+        if (hipMemsetAsync(A.flag_n, 0, sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
         hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap, 2.f,
                            (__bf16*)A.qbf, (int32_t*)A.qn);
         hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * tcap + 3) / 4), dim3(256), 0, st, t, nt, B, tcap, 1.f,

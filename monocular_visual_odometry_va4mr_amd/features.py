@@ -119,8 +119,9 @@ def bf_knn2_batch(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.
     B, qcap, tcap = int(q.shape[0]), int(q.shape[1]), int(t.shape[1])
     q = q.contiguous()
     t = t.contiguous()
-    idx2 = torch.full((B, qcap, 2), -1, dtype=torch.int32, device=dev)
-    dist2 = torch.full((B, qcap, 2), float(np.finfo(np.float32).max), dtype=torch.float32, device=dev)
+    # every entry is written by the call (absent pairs as -1 / FLT_MAX)
+    idx2 = torch.empty((B, qcap, 2), dtype=torch.int32, device=dev)
+    dist2 = torch.empty((B, qcap, 2), dtype=torch.float32, device=dev)
     lib = L.lib()
     nbytes = int(lib.vo_bf_knn2_batch_scratch(B, qcap, tcap))
     if nbytes <= 0:
