@@ -94,9 +94,54 @@ VO_DEV Cplx c_div(Cplx a, Cplx b)
     return {(a.re * b.re + a.im * b.im) * t, (-a.re * b.im + a.im * b.re) * t};
 }
 
+// The sweep of solve_poly at degree 10 (the five-point polynomial's usual degree) with every loop
+// unrolled, so the roots and coefficients stay in registers: the runtime-bound loops indexed them
+// dynamically, which put both arrays in scratch memory (about 200 scratch loads per sweep, 300
+// sweeps per solve; the sweeps almost never reach maxDiff == 0).  Same operations, same order.
+VO_DEV void solve_poly10(const Cplx (&co)[11], Cplx (&roots)[10])
+{
+    for (int iter = 0; iter < 300; ++iter) {
+        double maxDiff = 0;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const Cplx p = roots[i];
+            Cplx num = co[10], denom = co[10];
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                num = c_add(c_mul(num, p), co[10 - j - 1]);
+                if (j != i) {
+                    Cplx d = c_sub(p, roots[j]);
+                    if (!(d.re == 0 && d.im == 0)) denom = c_mul(denom, d);
+                }
+            }
+            num = c_div(num, denom);
+            roots[i] = c_sub(p, num);
+            double a = sqrt(num.re * num.re + num.im * num.im);
+            if (a > maxDiff) maxDiff = a;
+        }
+        if (maxDiff <= 0) break;
+    }
+}
+
 // cv::solvePoly (Weierstrass iteration, 300 sweeps max)
 VO_DEV int solve_poly(const double* c_in, int n0, Cplx* roots)
 {
+    if (n0 == 10 && fabs(c_in[10]) + fabs(0.0) > DBL_EPSILON) {
+        Cplx co[11], r[10];
+#pragma unroll
+        for (int i = 0; i <= 10; ++i) { co[i].re = c_in[i]; co[i].im = 0; }
+        Cplx p = {1, 0}, rr = {1, 1};
+#pragma unroll
+        for (int i = 0; i < 10; ++i) { r[i] = p; p = c_mul(p, rr); }
+        solve_poly10(co, r);
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            if (fabs(r[i].im) < 1e-100) r[i].im = 0;
+            roots[i] = r[i];
+        }
+        return 10;
+    }
+
     Cplx co[11];
     for (int i = 0; i <= n0; ++i) { co[i].re = c_in[i]; co[i].im = 0; }
     int n = n0;
