@@ -32,27 +32,44 @@ constexpr MonoTab make_mono()
     return t;
 }
 
-__constant__ MonoTab MT = make_mono();
+constexpr MonoTab MTc = make_mono();
 
 struct Poly3 { double c[20]; };
 
 VO_DEV void p_zero(Poly3& p) { for (int i = 0; i < 20; ++i) p.c[i] = 0.0; }
-VO_DEV void p_mul(const Poly3& a, const Poly3& b, Poly3& out)
+VO_DEV void p_axpy(double s, const Poly3& a, Poly3& y) { for (int i = 0; i < 20; ++i) y.c[i] += s * a.c[i]; }
+
+// The oracle's p_mul (oracle/vo_oracle_geom.c) over the operands' structural supports only
+// (D = 1: the linear polynomials of the null space, monomials x, y, z, 1; D = 2: their products,
+// every monomial of degree <= 2), fully
+// unrolled with the product table resolved at compile time, so no array is indexed at run time
+// (the loop over all 20 x 20 index pairs kept its operands in scratch memory; k_essential 2.59 ->
+// 2.15 ms per call at 32 chains).  Every entry outside a support is exactly zero, which p_mul
+// skips, and the supports are visited in ascending order: the same additions in the same order.
+template <int DA, int DB>
+VO_DEV void p_mul_s(const Poly3& a, const Poly3& b, Poly3& out)
 {
+    constexpr int S1[4] = {12, 15, 18, 19};
+    constexpr int S2[10] = {5, 7, 9, 11, 12, 14, 15, 17, 18, 19};
+    constexpr int NA = DA == 1 ? 4 : 10, NB = DB == 1 ? 4 : 10;
     Poly3 r;
-    p_zero(r);
-    for (int i = 0; i < 20; ++i) {
-        if (a.c[i] == 0.0) continue;
-        for (int j = 0; j < 20; ++j) {
-            if (b.c[j] == 0.0) continue;
-            const int k = MT.prod[i][j];
+#pragma unroll
+    for (int k = 0; k < 20; ++k) r.c[k] = 0.0;
+#pragma unroll
+    for (int ii = 0; ii < NA; ++ii) {
+        const int i = DA == 1 ? S1[ii] : S2[ii];
+        const double ai = a.c[i];
+#pragma unroll
+        for (int jj = 0; jj < NB; ++jj) {
+            const int j = DB == 1 ? S1[jj] : S2[jj];
+            const int k = MTc.prod[i][j];
             if (k < 0) continue;
-            r.c[k] += a.c[i] * b.c[j];
+            const double bj = b.c[j];
+            if (ai != 0.0 && bj != 0.0) r.c[k] += ai * bj;
         }
     }
     out = r;
 }
-VO_DEV void p_axpy(double s, const Poly3& a, Poly3& y) { for (int i = 0; i < 20; ++i) y.c[i] += s * a.c[i]; }
 
 VO_DEV int gauss_solve(double* A, int n, double* B, int m)
 {
@@ -225,24 +242,28 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
         p_zero(acc);
         const int cof[3][4] = {{4, 8, 5, 7}, {3, 8, 5, 6}, {3, 7, 4, 6}};
         const double sg[3] = {1, -1, 1};
+        #pragma unroll
         for (int c = 0; c < 3; ++c) {
             Poly3 m1, m2;
-            p_mul(Ep[cof[c][0]], Ep[cof[c][1]], m1);
-            p_mul(Ep[cof[c][2]], Ep[cof[c][3]], m2);
+            p_mul_s<1, 1>(Ep[cof[c][0]], Ep[cof[c][1]], m1);
+            p_mul_s<1, 1>(Ep[cof[c][2]], Ep[cof[c][3]], m2);
             p_axpy(-1.0, m2, m1);
-            p_mul(Ep[c], m1, t1);
+            p_mul_s<1, 2>(Ep[c], m1, t1);
             p_axpy(sg[c], t1, acc);
         }
         for (int c = 0; c < 20; ++c) { if (c < 10) A[c] = acc.c[c]; else Bm[c - 10] = acc.c[c]; }
     }
     {
         Poly3 EEt[9];
+        #pragma unroll
         for (int i = 0; i < 3; ++i)
+            #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 p_zero(EEt[i * 3 + j]);
+                #pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     Poly3 m;
-                    p_mul(Ep[i * 3 + k], Ep[j * 3 + k], m);
+                    p_mul_s<1, 1>(Ep[i * 3 + k], Ep[j * 3 + k], m);
                     p_axpy(1.0, m, EEt[i * 3 + j]);
                 }
             }
@@ -251,15 +272,18 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
         p_axpy(1.0, EEt[0], tr);
         p_axpy(1.0, EEt[4], tr);
         p_axpy(1.0, EEt[8], tr);
+        #pragma unroll
         for (int i = 0; i < 3; ++i)
+            #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 Poly3 acc, m;
                 p_zero(acc);
+                #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    p_mul(EEt[i * 3 + k], Ep[k * 3 + j], m);
+                    p_mul_s<2, 1>(EEt[i * 3 + k], Ep[k * 3 + j], m);
                     p_axpy(2.0, m, acc);
                 }
-                p_mul(tr, Ep[i * 3 + j], m);
+                p_mul_s<2, 1>(tr, Ep[i * 3 + j], m);
                 p_axpy(-1.0, m, acc);
                 const int r = 1 + i * 3 + j;
                 for (int c = 0; c < 20; ++c) { if (c < 10) A[r * 10 + c] = acc.c[c]; else Bm[r * 10 + (c - 10)] = acc.c[c]; }
