@@ -772,45 +772,59 @@ struct TriArgs {
     int force;
 };
 
-VO_DEV void triangulate_block(const TriArgs& A)
+// Shared per-chain context of the triangulation passes: the current pose (R_CW, t_CW), its
+// inverse and projection matrix, computed by thread 0.
+struct TriShared {
+    double Rc[9], tc[3], Rcwc[9], tcwc[3], Pc[12];
+    int fail, m;
+};
+
+// false: the chain does not triangulate this step (status set, or :366's nC <= 1)
+VO_DEV bool tri_setup(const TriArgs& A, TriShared& sh)
 {
-    __shared__ int lds[16];
-    __shared__ double Rc[9], tc[3], Rcwc[9], tcwc[3], Pc[12];
-    __shared__ int sh_fail, sh_m;
+    const int b = blockIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    if (s.status[b] != 0) return false;
+    if (!A.force && s.nC[b] <= 1) return false;                       // :366
+    if (threadIdx.x == 0) {
+        const int nF = s.nF[b];
+        const double* poseR = s.pose_R + (int64_t)b * d.fcap * 9;
+        const double* poset = s.pose_t + (int64_t)b * d.fcap * 3;
+        sh.fail = 0;
+        sh.m = 0;
+        // current pose (R_CW, t_CW) is slot nF; (R_WC, t_WC) = (R^T, -R^T t)
+        for (int i = 0; i < 9; ++i) sh.Rc[i] = poseR[(int64_t)nF * 9 + i];
+        for (int i = 0; i < 3; ++i) sh.tc[i] = poset[(int64_t)nF * 3 + i];
+        pose_inverse(sh.Rc, sh.tc, nF, sh.Rcwc, sh.tcwc);
+        proj_matrix(A.K, sh.Rcwc, sh.tcwc, sh.Pc);
+    }
+    __syncthreads();
+    return true;
+}
+
+// Three passes over the candidates (results identical to one pass, the reference's loop
+// :171-206): (1) the frame gate and check_baseline, listing the candidates that reach
+// cv2.triangulatePoints; (2) the triangulations, one listed candidate per thread -- the 4x4
+// Jacobi SVD is a long serial FP64 chain, so a chunk of 256 candidates with a few of them
+// triangulating cost as much as a chunk of 256 triangulations; (3) the ordered append /
+// compaction.  Scratch: the list, flags and list length in iwork, the points in work (PnP is
+// done with it).  The engine's step runs the three in the PnP block (k_pnp_tri); vo_triangulate
+// runs pass 2 over several blocks per chain (k_tri_solve).
+VO_DEV void tri_gate(const TriArgs& A, TriShared& sh)
+{
     const int b = blockIdx.x, tid = threadIdx.x;
     const vo_dims& d = A.d;
     const vo_state& s = A.s;
-    if (s.status[b] != 0) return;
-    const int nC = s.nC[b];
-    if (!A.force && nC <= 1) return;                                  // :366
-    const int nF = s.nF[b];
+    const int nC = s.nC[b], nF = s.nF[b];
     const double* poseR = s.pose_R + (int64_t)b * d.fcap * 9;
-    const double* poset = s.pose_t + (int64_t)b * d.fcap * 3;
-    if (tid == 0) {
-        sh_fail = 0;
-        sh_m = 0;
-        // current pose (R_CW, t_CW) is slot nF; (R_WC, t_WC) = (R^T, -R^T t)
-        for (int i = 0; i < 9; ++i) Rc[i] = poseR[(int64_t)nF * 9 + i];
-        for (int i = 0; i < 3; ++i) tc[i] = poset[(int64_t)nF * 3 + i];
-        pose_inverse(Rc, tc, nF, Rcwc, tcwc);
-        proj_matrix(A.K, Rcwc, tcwc, Pc);
-    }
-    __syncthreads();
-    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
-    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
-    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
-    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
-    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
-    // Three passes over the candidates (results identical to one pass, the reference's loop
-    // :171-206): (1) the frame gate and check_baseline, listing the candidates that reach
-    // cv2.triangulatePoints; (2) the triangulations, one listed candidate per thread -- the 4x4
-    // Jacobi SVD is a long serial FP64 chain, so a chunk of 256 candidates with a few of them
-    // triangulating cost as much as a chunk of 256 triangulations; (3) the ordered append /
-    // compaction.  Scratch: the list and flags in iwork, the points in work (PnP is done with it).
+    const float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    const float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    const int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
     const int kmax = d.ncap > d.pcap ? d.ncap : d.pcap;
     int32_t* tlist = s.iwork + (int64_t)b * d.iwork_stride;          // [m] candidate indices
     int32_t* tacc = tlist + kmax;                                      // [nC] 1 = becomes a landmark
-    float* tX = (float*)(s.work + (int64_t)b * d.work_stride);          // [nC][3] its point
+    const double* Rc = sh.Rc;
     for (int i = tid; i < nC; i += blockDim.x) {
         const float k0 = ck[2 * i], k1 = ck[2 * i + 1], f0 = cf[2 * i], f1 = cf[2 * i + 1];
         const int tau = ct[i];
@@ -841,11 +855,28 @@ VO_DEV void triangulate_block(const TriArgs& A)
             tri = !(cs >= A.cos_thr);                                   // else retained
         }
         tacc[i] = 0;
-        if (tri) tlist[atomicAdd(&sh_m, 1)] = i;
+        if (tri) tlist[atomicAdd(&sh.m, 1)] = i;
     }
     __syncthreads();
-    const int m = sh_m;
-    for (int j = tid; j < m; j += blockDim.x) {
+}
+
+// pass 2 over list entries j0, j0 + stride, ... (m entries)
+VO_DEV void tri_solve(const TriArgs& A, const TriShared& sh, int m, int j0, int stride)
+{
+    const int b = blockIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    const int nF = s.nF[b];
+    const double* poseR = s.pose_R + (int64_t)b * d.fcap * 9;
+    const double* poset = s.pose_t + (int64_t)b * d.fcap * 3;
+    const float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    const float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    const int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    const int kmax = d.ncap > d.pcap ? d.ncap : d.pcap;
+    const int32_t* tlist = s.iwork + (int64_t)b * d.iwork_stride;
+    int32_t* tacc = s.iwork + (int64_t)b * d.iwork_stride + kmax;
+    float* tX = (float*)(s.work + (int64_t)b * d.work_stride);          // [nC][3] its point
+    for (int j = j0; j < m; j += stride) {
         const int i = tlist[j];
         const float k0 = ck[2 * i], k1 = ck[2 * i + 1], f0 = cf[2 * i], f1 = cf[2 * i + 1];
         const int tau = ct[i];
@@ -855,20 +886,37 @@ VO_DEV void triangulate_block(const TriArgs& A)
         pose_inverse(Rp, tp, tau, Rpw, tpw);
         proj_matrix(A.K, Rpw, tpw, Pp);
         double X4[4];
-        tri_one(Pp, Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
+        tri_one(Pp, sh.Pc, (double)f0, (double)f1, (double)k0, (double)k1, X4);
         const float w4 = (float)X4[3];
         float Xo[3];
         Xo[0] = (float)X4[0] / w4;
         Xo[1] = (float)X4[1] / w4;
         Xo[2] = (float)X4[2] / w4;
-        const double zc = depth_of(Rcwc, tcwc, nF, Xo);
+        const double zc = depth_of(sh.Rcwc, sh.tcwc, nF, Xo);
         const double zp = depth_of(Rpw, tpw, tau, Xo);
         if (zc > A.min_d && zp > A.min_d && zc < A.max_d && zp < A.max_d) {
             tacc[i] = 1;
             tX[3 * i] = Xo[0]; tX[3 * i + 1] = Xo[1]; tX[3 * i + 2] = Xo[2];
         }                                                               // else retained (quirk Q5)
     }
-    __syncthreads();
+}
+
+// pass 3: ordered append of the accepted candidates to the landmarks, in-place compaction of the rest
+VO_DEV void tri_append(const TriArgs& A, TriShared& sh)
+{
+    __shared__ int lds[16];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    const int nC = s.nC[b];
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    const int kmax = d.ncap > d.pcap ? d.ncap : d.pcap;
+    const int32_t* tacc = s.iwork + (int64_t)b * d.iwork_stride + kmax;
+    const float* tX = (const float*)(s.work + (int64_t)b * d.work_stride);
     int nL = s.nL[b];
     int kept = 0;
     for (int base = 0; base < nC; base += blockDim.x) {
@@ -890,7 +938,7 @@ VO_DEV void triangulate_block(const TriArgs& A)
                 X[3 * pa] = tX[3 * i]; X[3 * pa + 1] = tX[3 * i + 1]; X[3 * pa + 2] = tX[3 * i + 2];
                 kp[2 * pa] = k0; kp[2 * pa + 1] = k1;
             } else {
-                sh_fail = 1;
+                sh.fail = 1;
             }
         } else if (valid) {
             const int pr = kept + (tid - pre);
@@ -903,11 +951,51 @@ VO_DEV void triangulate_block(const TriArgs& A)
     if (tid == 0) {
         s.nL[b] = nL < d.ncap ? nL : d.ncap;
         s.nC[b] = kept;
-        if (sh_fail) s.status[b] = VO_ST_CAPACITY;
+        if (sh.fail) s.status[b] = VO_ST_CAPACITY;
     }
 }
 
+VO_DEV void triangulate_block(const TriArgs& A)
+{
+    __shared__ TriShared sh;
+    if (!tri_setup(A, sh)) return;
+    tri_gate(A, sh);
+    tri_solve(A, sh, sh.m, threadIdx.x, blockDim.x);
+    __syncthreads();
+    tri_append(A, sh);
+}
+
 __global__ void __launch_bounds__(256) k_triangulate(TriArgs A) { triangulate_block(A); }
+
+// vo_triangulate as three launches: the gate (one block per chain, list length into iwork), the
+// triangulations over TRI_SPLIT blocks per chain, the ordered append (one block per chain).  With
+// few chains the one-block form left most CUs idle while each block ran ~12 serial 4x4 SVDs per
+// thread (the bootstrap's ~3,000 candidates per chain).
+#define TRI_SPLIT 8
+__global__ void __launch_bounds__(256) k_tri_gate(TriArgs A)
+{
+    __shared__ TriShared sh;
+    if (!tri_setup(A, sh)) return;
+    tri_gate(A, sh);
+    if (threadIdx.x == 0) {
+        const int kmax = A.d.ncap > A.d.pcap ? A.d.ncap : A.d.pcap;
+        A.s.iwork[(int64_t)blockIdx.x * A.d.iwork_stride + 2 * kmax] = sh.m;
+    }
+}
+__global__ void __launch_bounds__(256) k_tri_solve(TriArgs A)
+{
+    __shared__ TriShared sh;
+    if (!tri_setup(A, sh)) return;
+    const int kmax = A.d.ncap > A.d.pcap ? A.d.ncap : A.d.pcap;
+    const int m = A.s.iwork[(int64_t)blockIdx.x * A.d.iwork_stride + 2 * kmax];
+    tri_solve(A, sh, m, blockIdx.y * blockDim.x + threadIdx.x, gridDim.y * blockDim.x);
+}
+__global__ void __launch_bounds__(256) k_tri_append(TriArgs A)
+{
+    __shared__ TriShared sh;
+    if (!tri_setup(A, sh)) return;
+    tri_append(A, sh);
+}
 
 // vo_pnp + vo_triangulate(force 0) as one launch (the engine's step): the triangulation of a
 // chain runs in the block that just solved its pose, instead of waiting for CUs again
@@ -1146,7 +1234,16 @@ extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state
     if (!d || !o || !s) return VO_EARG;
     TriArgs A;
     fill_tri(A, d, o, s, force);
-    hipLaunchKernelGGL(k_triangulate, dim3(d->B), dim3(256), 0, VO_STREAM(stream), A);
+    const int kmax = d->ncap > d->pcap ? d->ncap : d->pcap;
+    if (d->iwork_stride < 2LL * kmax + 1) return VO_EARG;
+    hipStream_t st = VO_STREAM(stream);
+    if (d->B >= (device_cus() > 0 ? device_cus() : 256)) {
+        hipLaunchKernelGGL(k_triangulate, dim3(d->B), dim3(256), 0, st, A);
+    } else {
+        hipLaunchKernelGGL(k_tri_gate, dim3(d->B), dim3(256), 0, st, A);
+        hipLaunchKernelGGL(k_tri_solve, dim3(d->B, TRI_SPLIT), dim3(256), 0, st, A);
+        hipLaunchKernelGGL(k_tri_append, dim3(d->B), dim3(256), 0, st, A);
+    }
     return hip_rc();
 }
 
