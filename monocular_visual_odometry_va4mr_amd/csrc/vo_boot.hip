@@ -520,38 +520,36 @@ struct RecArgs {
     int sign_fix;            // apply t *= sign(t_z) (VisualOdometryPipeLine.py:317)
 };
 
-__global__ void __launch_bounds__(256) k_recover_pose(RecArgs A)
+// recoverPose's two rotations and translation from E (thread 0; the block's shared copies)
+VO_DEV void rp_decompose(const double* E, double* R1, double* R2, double* tt)
 {
-    __shared__ double R1[9], R2[9], tt[3];
-    __shared__ int lds[16];
-    __shared__ int good[4];
-    const int b = blockIdx.x, tid = threadIdx.x;
-    if (A.chain_status && A.chain_status[b] != 0) return;
-    const int n = A.counts[b];
+    double U[9], w[3], V[9];
+    for (int q = 0; q < 9; ++q) U[q] = E[q];
+    svd_jacobi<3, 3>(U, w, V);
+    if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
+    if (det3(V) < 0) for (int i = 0; i < 9; ++i) V[i] = -V[i];
+    const double W[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1}, Wt[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
+    double Vt[9], UW[9];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Vt[i * 3 + j] = V[j * 3 + i];
+    matmul3(U, W, UW);
+    matmul3(UW, Vt, R1);
+    matmul3(U, Wt, UW);
+    matmul3(UW, Vt, R2);
+    for (int i = 0; i < 3; ++i) tt[i] = U[i * 3 + 2];
+}
+
+// the four-way cheirality test of points i0, i0 + stride, ... (< n): per-candidate counts in g,
+// per-point bits in mask (if non-null)
+VO_DEV void rp_count(const RecArgs& A, const double* R1, const double* R2, const double* tt, int n, int i0,
+                     int stride, int (&g)[4], uint8_t* mask)
+{
+    const int b = blockIdx.x;
     const float* p0 = A.p0 + (int64_t)b * A.cap * 2;
     const float* p1 = A.p1 + (int64_t)b * A.cap * 2;
     const double fx = A.K[0], fy = A.K[4], cx = A.K[2], cy = A.K[5];
-    if (tid == 0) {
-        double U[9], w[3], V[9];
-        for (int q = 0; q < 9; ++q) U[q] = A.E[9 * b + q];
-        svd_jacobi<3, 3>(U, w, V);
-        if (det3(U) < 0) for (int i = 0; i < 9; ++i) U[i] = -U[i];
-        if (det3(V) < 0) for (int i = 0; i < 9; ++i) V[i] = -V[i];
-        const double W[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1}, Wt[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
-        double Vt[9], UW[9];
-        for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Vt[i * 3 + j] = V[j * 3 + i];
-        matmul3(U, W, UW);
-        matmul3(UW, Vt, R1);
-        matmul3(U, Wt, UW);
-        matmul3(UW, Vt, R2);
-        for (int i = 0; i < 3; ++i) tt[i] = U[i * 3 + 2];
-    }
-    __syncthreads();
     const double dist = 50.0;
     const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-    int g[4] = {0, 0, 0, 0};
-    uint8_t* mask = A.mask ? A.mask + (int64_t)b * A.cap : nullptr;
-    for (int i = tid; i < n; i += blockDim.x) {
+    for (int i = i0; i < n; i += stride) {
         const double x1 = ((double)p0[2 * i] - cx) / fx, y1 = ((double)p0[2 * i + 1] - cy) / fy;
         const double x2 = ((double)p1[2 * i] - cx) / fx, y2 = ((double)p1[2 * i + 1] - cy) / fy;
         uint8_t bits = 0;
@@ -578,19 +576,17 @@ __global__ void __launch_bounds__(256) k_recover_pose(RecArgs A)
         }
         if (mask) mask[i] = bits;
     }
-    for (int c = 0; c < 4; ++c) {
-        const int s = block_sum_i32(g[c], lds);
-        if (tid == 0) good[c] = s;
-    }
-    __syncthreads();
-    int sel;
+}
+
+// the candidate with the most points in front of both cameras (first of equals), its R and t
+VO_DEV void rp_pick(const RecArgs& A, const int* good, const double* R1, const double* R2, const double* tt, int& sel)
+{
+    const int b = blockIdx.x;
     if (good[0] >= good[1] && good[0] >= good[2] && good[0] >= good[3]) sel = 0;
     else if (good[1] >= good[0] && good[1] >= good[2] && good[1] >= good[3]) sel = 1;
     else if (good[2] >= good[0] && good[2] >= good[1] && good[2] >= good[3]) sel = 2;
     else sel = 3;
-    if (mask)
-        for (int i = tid; i < n; i += blockDim.x) mask[i] = (mask[i] >> sel) & 1;
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         const double* Rs = (sel == 0 || sel == 2) ? R1 : R2;
         double t3[3];
         for (int i = 0; i < 3; ++i) t3[i] = (sel < 2) ? tt[i] : -tt[i];
@@ -604,15 +600,73 @@ __global__ void __launch_bounds__(256) k_recover_pose(RecArgs A)
     }
 }
 
+__global__ void __launch_bounds__(256) k_recover_pose(RecArgs A)
+{
+    __shared__ double R1[9], R2[9], tt[3];
+    __shared__ int lds[16];
+    __shared__ int good[4];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (A.chain_status && A.chain_status[b] != 0) return;
+    const int n = A.counts[b];
+    if (tid == 0) rp_decompose(A.E + 9 * b, R1, R2, tt);
+    __syncthreads();
+    int g[4] = {0, 0, 0, 0};
+    uint8_t* mask = A.mask ? A.mask + (int64_t)b * A.cap : nullptr;
+    rp_count(A, R1, R2, tt, n, tid, blockDim.x, g, mask);
+    for (int c = 0; c < 4; ++c) {
+        const int s = block_sum_i32(g[c], lds);
+        if (tid == 0) good[c] = s;
+    }
+    __syncthreads();
+    int sel;
+    rp_pick(A, good, R1, R2, tt, sel);
+    if (mask)
+        for (int i = tid; i < n; i += blockDim.x) mask[i] = (mask[i] >> sel) & 1;
+}
+
+// The bootstrap's recoverPose (no mask output) with few chains: the cheirality counts over
+// RP_SPLIT blocks per chain (integer sums, order-free) into gcount [B][4] (zeroed by
+// k_boot_apply), then the pick by one block per chain.  One block per chain left most CUs idle
+// while each thread triangulated ~12 points four ways.
+#define RP_SPLIT 8
+__global__ void __launch_bounds__(256) k_recover_count(RecArgs A, int32_t* gcount)
+{
+    __shared__ double R1[9], R2[9], tt[3];
+    __shared__ int lds[16];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    if (A.chain_status && A.chain_status[b] != 0) return;
+    const int n = A.counts[b];
+    if (tid == 0) rp_decompose(A.E + 9 * b, R1, R2, tt);
+    __syncthreads();
+    int g[4] = {0, 0, 0, 0};
+    rp_count(A, R1, R2, tt, n, blockIdx.y * blockDim.x + tid, gridDim.y * blockDim.x, g, nullptr);
+    for (int c = 0; c < 4; ++c) {
+        const int s = block_sum_i32(g[c], lds);
+        if (tid == 0 && s) atomicAdd(&gcount[4 * b + c], s);
+    }
+}
+__global__ void __launch_bounds__(64) k_recover_pick(RecArgs A, const int32_t* gcount)
+{
+    __shared__ double R1[9], R2[9], tt[3];
+    const int b = blockIdx.x;
+    if (A.chain_status && A.chain_status[b] != 0) return;
+    if (threadIdx.x == 0) rp_decompose(A.E + 9 * b, R1, R2, tt);
+    __syncthreads();
+    const int good[4] = {gcount[4 * b], gcount[4 * b + 1], gcount[4 * b + 2], gcount[4 * b + 3]};
+    int sel;
+    rp_pick(A, good, R1, R2, tt, sel);
+}
+
 // ------------------------------------------------------------------ bootstrap assembly
 // initialization :306-313: candidates <- matches, E-inlier split, filter_potential
 __global__ void __launch_bounds__(256) k_boot_apply(vo_dims d, vo_state s, const float* pts0, const float* pts1,
                                                     const int32_t* counts, int cap, const uint8_t* emask,
-                                                    const int32_t* eok)
+                                                    const int32_t* eok, int32_t* gcount)
 {
     __shared__ int lds[16];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int n = counts[b];
+    if (tid < 4) gcount[4 * b + tid] = 0;                              // k_recover_count's sums
     if (tid == 0) {
         s.status[b] = 0;
         s.nL[b] = 0;
@@ -744,19 +798,25 @@ extern "C" int vo_bootstrap(const vo_dims* d, const vo_opts* o, const vo_state* 
     double* Ebuf = (double*)s->trk_pts;
     double* Rbuf = Ebuf + 9 * (int64_t)d->B;
     double* tbuf = Rbuf + 9 * (int64_t)d->B;
+    int32_t* gcount = (int32_t*)(tbuf + 3 * (int64_t)d->B);                // [B][4]
     A.E = Ebuf;
     if (cap > d->ncap) return VO_EARG;            // the E mask lives in pnp_mask [B][ncap]
     A.mask = s->pnp_mask;
     A.cap = cap;
     launch_essential(A, d->B, st);
     hipLaunchKernelGGL(k_boot_apply, dim3(d->B), dim3(256), 0, st, *d, *s, pts0, pts1, counts, cap,
-                       (const uint8_t*)s->pnp_mask, (const int32_t*)s->pnp_ok);
+                       (const uint8_t*)s->pnp_mask, (const int32_t*)s->pnp_ok, gcount);
     RecArgs Rg;
     for (int i = 0; i < 9; ++i) Rg.K[i] = o->K[i];
     Rg.E = Ebuf; Rg.p0 = s->c_first; Rg.p1 = s->c_kp; Rg.counts = s->nC; Rg.cap = d->pcap;
     Rg.R = Rbuf; Rg.t = tbuf; Rg.mask = nullptr; Rg.n_good = s->pnp_ninl; Rg.chain_status = s->status;
     Rg.sign_fix = 1;
-    hipLaunchKernelGGL(k_recover_pose, dim3(d->B), dim3(256), 0, st, Rg);
+    if (d->B >= (device_cus() > 0 ? device_cus() : 256)) {
+        hipLaunchKernelGGL(k_recover_pose, dim3(d->B), dim3(256), 0, st, Rg);
+    } else {
+        hipLaunchKernelGGL(k_recover_count, dim3(d->B, RP_SPLIT), dim3(256), 0, st, Rg, gcount);
+        hipLaunchKernelGGL(k_recover_pick, dim3(d->B), dim3(64), 0, st, Rg, (const int32_t*)gcount);
+    }
     hipLaunchKernelGGL(k_copy_pose, dim3((d->B + 63) / 64), dim3(64), 0, st, *d, *s, (const double*)Rbuf,
                        (const double*)tbuf);
     int rc = vo_triangulate(d, o, s, 1, stream);
