@@ -315,7 +315,7 @@ def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=2):
     res = None
     for _ in range(reps):
         r = run("kitti", SEQ_LEN, per_gpu, overlap=30, seed=seed, device=device, rank=rank, world=world,
-                reference=ref, time_boot=True, groups=groups)
+                reference=ref, time_boot=False, groups=groups)
         if r is not None and (res is None or r["wall_s"] < res["wall_s"]):
             res = r
         torch.cuda.empty_cache()

@@ -141,6 +141,13 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
             with on(g):
                 eng.reserve_bootstrap()
     _sync(dev)
+    # without time_boot the groups are not synchronised after their bootstraps (a group steps
+    # as soon as its own bootstrap is done); the bootstrap time is then the latest group's
+    # end-of-bootstrap event
+    ev0 = ev_boot = None
+    if not time_boot and cuda:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(torch.cuda.current_stream(dev))
     t0 = time.perf_counter()
     if G > 1 and cuda:
         for st in streams:
@@ -148,6 +155,12 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     for g, eng in enumerate(engines):
         with on(g):
             eng.bootstrap(boot0[bounds[g]:bounds[g + 1]], boot1[bounds[g]:bounds[g + 1]])
+            if ev0 is not None:
+                if ev_boot is None:
+                    ev_boot = []
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(torch.cuda.current_stream(dev))
+                ev_boot.append(e)
     if time_boot:
         _sync(dev)
     t_boot = time.perf_counter() - t0
@@ -175,6 +188,8 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     host_s = time.perf_counter() - t0
     _sync(dev)
     wall = time.perf_counter() - t0
+    if ev_boot:
+        t_boot = max(ev0.elapsed_time(e) for e in ev_boot) / 1e3
     t_step = wall - t_boot
     final_status = torch.cat(final_status)
     for eng in engines:

@@ -1,6 +1,6 @@
 """Sweep of the whole-sequence job (C2, 4541 frames) over the shards per GPU.
 
-    python tools/seq_sweep.py [B ...] [--groups G,G]
+    python tools/seq_sweep.py [B ...] [--groups G,G] [--reps R] [--no-boot-sync]
 
 For each B: the sequence cut into B shards (30-frame overlap) run as the B chains of one engine
 on this GPU (run_sequence.run), bootstrap timed separately; prints one JSON line per B with
@@ -34,6 +34,8 @@ def main():
         i = argv.index("--groups")
         Gs = [int(g) for g in argv[i + 1].split(",")]
         argv = argv[:i] + argv[i + 2:]
+    boot_sync = "--no-boot-sync" not in argv
+    argv = [a for a in argv if a != "--no-boot-sync"]
     Bs = [int(a) for a in argv] or [16, 32, 64, 128, 256]
     dev = torch.device("cuda", 0)
     gold = os.path.join(ROOT, "tests", "golden", "kitti_seq00_shards.npz")
@@ -43,7 +45,7 @@ def main():
         best = None
         for rep in range(reps):
             t0 = time.perf_counter()
-            r = run("kitti", 4541, B, overlap=30, seed=1, device=dev, reference=ref, time_boot=True,
+            r = run("kitti", 4541, B, overlap=30, seed=1, device=dev, reference=ref, time_boot=boot_sync,
                     prerender=True, groups=G)
             tot = time.perf_counter() - t0
             if best is None or r["wall_s"] < best["wall_s"]:
