@@ -143,6 +143,10 @@ int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t str
  * to pyr[1-prev], then the reference's status filtering (ordered compaction). */
 int vo_track(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, vo_stream_t stream);
 
+/* vo_track without the filtering: the calcOpticalFlowPyrLK calls (:281, :287) into the tracking
+ * scratch (trk_pts, trk_st); vo_filter_pnp_triangulate then filters (:283-290) in its PnP block. */
+int vo_track_lk(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, vo_stream_t stream);
+
 /* PnP step (:338-358): guard N >= 8, cv2.solvePnPRansac(P3P) + EPnP refit, inlier
  * filtering, Rodrigues, inversion; writes pose slot nF (not yet counted). */
 int vo_pnp(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
@@ -156,6 +160,10 @@ int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int fo
  * block that solved its pose (the engine's step; same results as the two calls).  No reference
  * counterpart of its own: it replaces the pair VisualOdometryPipeLine.py:342-358 + :366-368. */
 int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
+
+/* feature_tracking's status filtering (:283-290) after vo_track_lk, then vo_pnp_triangulate, in
+ * one launch (the engine's step: one kernel boundary fewer between tracking and PnP). */
+int vo_filter_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream);
 
 /* cv2.goodFeaturesToTrack (:256) on pyramid level 0 of pyr[cur] -> state->corners. */
 int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, int cur, vo_stream_t stream);

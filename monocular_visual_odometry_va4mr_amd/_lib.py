@@ -131,9 +131,11 @@ def _declare(L):
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),
+        "vo_track_lk": ([D, O, S, C.c_int, P], C.c_int),
         "vo_pnp": ([D, O, S, P], C.c_int),
         "vo_triangulate": ([D, O, S, C.c_int, P], C.c_int),
         "vo_pnp_triangulate": ([D, O, S, P], C.c_int),
+        "vo_filter_pnp_triangulate": ([D, O, S, P], C.c_int),
         "vo_gftt": ([D, O, S, C.c_int, P], C.c_int),
         "vo_gftt_eigmap": ([D, O, S, C.c_int, P], C.c_int),
         "vo_add_corners_finish": ([D, O, S, P], C.c_int),

@@ -215,3 +215,51 @@ static inline int device_cus()
     if (dev < 64) cache[dev] = n;
     return n;
 }
+
+// feature_tracking's filtering (VisualOdometryPipeLine.py:283-290) for chain blockIdx.x: the
+// tracked landmarks and candidates with status 1, in order (ordered compaction from the tracking
+// scratch trk_pts / trk_st)
+VO_DEV void track_compact_block(const vo_dims& d, const vo_state& s)
+{
+    __shared__ int lds[16];
+    const int b = blockIdx.x;
+    if (s.status[b] != 0) return;
+    const int nL = s.nL[b], nC = s.nC[b];
+    const int ocap = d.ncap + d.pcap;
+    const float* tp = s.trk_pts + (int64_t)b * ocap * 2;
+    const uint8_t* ts = s.trk_st + (int64_t)b * ocap;
+    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+    int out = 0;
+    for (int base = 0; base < nL; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool ok = i < nL && ts[i] == 1;
+        float x0 = 0, x1 = 0, x2 = 0, k0 = 0, k1 = 0;
+        if (ok) { x0 = X[3 * i]; x1 = X[3 * i + 1]; x2 = X[3 * i + 2]; k0 = tp[2 * i]; k1 = tp[2 * i + 1]; }
+        int tot;
+        const int pos = out + block_scan_flag(ok, lds, &tot);
+        if (ok) { X[3 * pos] = x0; X[3 * pos + 1] = x1; X[3 * pos + 2] = x2; kp[2 * pos] = k0; kp[2 * pos + 1] = k1; }
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s.nL[b] = out;
+    if (nC <= 1) return;   // quirk Q7: a single candidate is neither tracked nor filtered
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    out = 0;
+    for (int base = 0; base < nC; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool ok = i < nC && ts[nL + i] == 1;
+        float k0 = 0, k1 = 0, f0 = 0, f1 = 0;
+        int tau = 0;
+        if (ok) { k0 = tp[2 * (nL + i)]; k1 = tp[2 * (nL + i) + 1]; f0 = cf[2 * i]; f1 = cf[2 * i + 1]; tau = ct[i]; }
+        int tot;
+        const int pos = out + block_scan_flag(ok, lds, &tot);
+        if (ok) { ck[2 * pos] = k0; ck[2 * pos + 1] = k1; cf[2 * pos] = f0; cf[2 * pos + 1] = f1; ct[pos] = tau; }
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) s.nC[b] = out;
+}
+

@@ -1046,49 +1046,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 }
 
 // ---------------------------------------------------- tracking compaction (:282-290)
-__global__ void __launch_bounds__(256) k_track_compact(vo_dims d, vo_state s)
-{
-    __shared__ int lds[16];
-    const int b = blockIdx.x;
-    if (s.status[b] != 0) return;
-    const int nL = s.nL[b], nC = s.nC[b];
-    const int ocap = d.ncap + d.pcap;
-    const float* tp = s.trk_pts + (int64_t)b * ocap * 2;
-    const uint8_t* ts = s.trk_st + (int64_t)b * ocap;
-    float* X = s.lm_X + (int64_t)b * d.ncap * 3;
-    float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
-    int out = 0;
-    for (int base = 0; base < nL; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const bool ok = i < nL && ts[i] == 1;
-        float x0 = 0, x1 = 0, x2 = 0, k0 = 0, k1 = 0;
-        if (ok) { x0 = X[3 * i]; x1 = X[3 * i + 1]; x2 = X[3 * i + 2]; k0 = tp[2 * i]; k1 = tp[2 * i + 1]; }
-        int tot;
-        const int pos = out + block_scan_flag(ok, lds, &tot);
-        if (ok) { X[3 * pos] = x0; X[3 * pos + 1] = x1; X[3 * pos + 2] = x2; kp[2 * pos] = k0; kp[2 * pos + 1] = k1; }
-        out += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) s.nL[b] = out;
-    if (nC <= 1) return;   // quirk Q7: a single candidate is neither tracked nor filtered
-    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
-    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
-    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
-    out = 0;
-    for (int base = 0; base < nC; base += blockDim.x) {
-        const int i = base + threadIdx.x;
-        const bool ok = i < nC && ts[nL + i] == 1;
-        float k0 = 0, k1 = 0, f0 = 0, f1 = 0;
-        int tau = 0;
-        if (ok) { k0 = tp[2 * (nL + i)]; k1 = tp[2 * (nL + i) + 1]; f0 = cf[2 * i]; f1 = cf[2 * i + 1]; tau = ct[i]; }
-        int tot;
-        const int pos = out + block_scan_flag(ok, lds, &tot);
-        if (ok) { ck[2 * pos] = k0; ck[2 * pos + 1] = k1; cf[2 * pos] = f0; cf[2 * pos + 1] = f1; ct[pos] = tau; }
-        out += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) s.nC[b] = out;
-}
+// feature_tracking's status filtering (:283-290) as its own launch (vo_track); the engine's
+// step runs the same block function at the start of the PnP block (vo_filter_pnp_triangulate)
+__global__ void __launch_bounds__(256) k_track_compact(vo_dims d, vo_state s) { track_compact_block(d, s); }
 
 // ------------------------------------------------------------------ GFTT
 struct EigParams {
@@ -2077,6 +2037,18 @@ extern "C" int vo_track(const vo_dims* d, const vo_opts* o, const vo_state* s, i
     if (rc) return rc;
     hipLaunchKernelGGL(k_track_compact, dim3(d->B), dim3(256), 0, VO_STREAM(stream), *d, *s);
     return hip_ok() ? VO_OK : VO_EHIP;
+}
+
+extern "C" int vo_track_lk(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, vo_stream_t stream)
+{
+    if (!d || !o || !s || prev < 0 || prev > 1) return VO_EARG;
+    LKParams P;
+    fill_lk(P, d, o, s, prev);
+    P.p0 = s->lm_kp; P.n0 = s->nL; P.cap0 = d->ncap;
+    P.p1 = s->c_kp; P.n1 = s->nC; P.cap1 = d->pcap; P.seg1_min = 1;   // :286 "if P > 1"
+    P.chain_status = s->status;
+    P.out = s->trk_pts; P.st = s->trk_st; P.err = s->trk_err; P.ocap = d->ncap + d->pcap;
+    return launch_lk(P, d->B, VO_STREAM(stream));
 }
 
 extern "C" int vo_lk_points(const vo_dims* d, const vo_opts* o, const vo_state* s, int prev, const float* pts,

@@ -770,6 +770,7 @@ struct TriArgs {
     double cos_thr;        // retain iff clip(cos) >= cos_thr  <=>  degrees(arccos(cos)) < min_baseline_angle
     int min_frames;
     int force;
+    int compact;           // k_pnp_tri: run feature_tracking's filtering first (vo_filter_pnp_triangulate)
 };
 
 // Shared per-chain context of the triangulation passes: the current pose (R_CW, t_CW), its
@@ -1003,6 +1004,10 @@ template <int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 k_pnp_tri(PnPArgs A, TriArgs T)
 {
+    if (T.compact) {                      // the tracking stage left the status filtering to us
+        track_compact_block(T.d, T.s);
+        __syncthreads();
+    }
     pnp_ransac_block(A);
     __syncthreads();
     pnp_apply_block(T.d, T.s, A.rvec, A.tvec, A.success, A.mask);
@@ -1227,6 +1232,7 @@ static void fill_tri(TriArgs& A, const vo_dims* d, const vo_opts* o, const vo_st
     A.cos_thr = o->cos_baseline;
     A.min_frames = o->min_baseline_frames;
     A.force = force;
+    A.compact = 0;
 }
 
 extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, int force, vo_stream_t stream)
@@ -1247,7 +1253,7 @@ extern "C" int vo_triangulate(const vo_dims* d, const vo_opts* o, const vo_state
     return hip_rc();
 }
 
-extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+static int launch_pnp_tri(const vo_dims* d, const vo_opts* o, const vo_state* s, int compact, vo_stream_t stream)
 {
     if (!d || !o || !s) return VO_EARG;
     if (d->work_stride < 12LL * d->ncap + 64) return VO_EARG;
@@ -1255,6 +1261,7 @@ extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_s
     fill_pnp_engine(P, d, o, s);
     TriArgs T;
     fill_tri(T, d, o, s, 0);
+    T.compact = compact;
     // more chains than CUs: the 2-waves/SIMD build (two blocks per CU, some registers spilled);
     // otherwise every block has a CU of its own and the unconstrained build is faster
     // (VO_PNP_TRI_WPE=1|2 forces one build: measurement option)
@@ -1264,6 +1271,16 @@ extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_s
     if (two) hipLaunchKernelGGL(k_pnp_tri<VO_PNP_WPE>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     else hipLaunchKernelGGL(k_pnp_tri<1>, dim3(d->B), dim3(256), 0, VO_STREAM(stream), P, T);
     return hip_rc();
+}
+
+extern "C" int vo_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    return launch_pnp_tri(d, o, s, 0, stream);
+}
+
+extern "C" int vo_filter_pnp_triangulate(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)
+{
+    return launch_pnp_tri(d, o, s, 1, stream);
 }
 
 extern "C" int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const vo_state* s, vo_stream_t stream)

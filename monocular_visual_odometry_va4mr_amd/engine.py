@@ -14,6 +14,9 @@ The reference's per-frame control flow maps to stages as
     triangulation   :366-367    -> vo_triangulate
     feature_adding  :369        -> vo_gftt(cur) + vo_add_corners_finish (also :371-373)
 
+(by default the filtering of feature_tracking, PnP and triangulation run as one launch:
+vo_track_lk + vo_filter_pnp_triangulate; VO_PNP_TRI_SPLIT=1 selects the separate calls)
+
 and runtime ValueErrors of the reference become per-chain status codes (``statuses``).
 """
 from __future__ import annotations
@@ -309,7 +312,12 @@ class Engine:
             side.wait_stream(main)                                # pyramid(cur) ready
         if not gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
-        run(1, main, lambda: lib.vo_track(pd, po, ps, prev, sm))
+        fused = getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1")
+        # fused: tracking leaves the status filtering (:283-290) to the PnP launch, which runs it
+        # first in each chain's block (one kernel boundary fewer on the step's critical path)
+        defer = fused and os.environ.get("VO_COMPACT_IN_TRACK") != "1"      # =1: A/B option
+        track = lib.vo_track_lk if defer else lib.vo_track
+        run(1, main, lambda: track(pd, po, ps, prev, sm))
         if gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         lat = main
@@ -317,9 +325,11 @@ class Engine:
             lat = self._latency_stream()
             lat.wait_stream(main)                                 # tracking done
         sl = C.c_void_p(lat.cuda_stream)
-        if getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1"):
-            # one launch for both stages (vo_pnp_triangulate); stage 3 is then empty
-            run(2, lat, lambda: lib.vo_pnp_triangulate(pd, po, ps, sl))
+        if fused:
+            # one launch for filtering, PnP and triangulation (vo_filter_pnp_triangulate); stage 3
+            # is then empty
+            pnp = lib.vo_filter_pnp_triangulate if defer else lib.vo_pnp_triangulate
+            run(2, lat, lambda: pnp(pd, po, ps, sl))
             run(3, lat, lambda: 0)
         else:
             run(2, lat, lambda: lib.vo_pnp(pd, po, ps, sl))
