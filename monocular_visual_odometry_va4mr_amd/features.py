@@ -101,11 +101,17 @@ _SCRATCH: dict = {}
 
 
 def _scratch(dev, nbytes: int) -> torch.Tensor:
-    """Matcher scratch per device, grown on demand (kept so repeated calls do not allocate)."""
-    buf = _SCRATCH.get(dev)
+    """Matcher scratch per (device, stream), grown on demand (kept so repeated calls do not
+    allocate).  Per stream: engines bootstrapping concurrently on streams of their own (the
+    sequence job's stream groups, the headline's two engines) must not share it -- one shared
+    buffer per device let one group's match overwrite the other's staged rows (found in round 4
+    when the groups' bootstraps overlapped more: half the shards of one group differed from the
+    reference runs)."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _SCRATCH.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        _SCRATCH[dev] = buf
+        _SCRATCH[key] = buf
     return buf
 
 

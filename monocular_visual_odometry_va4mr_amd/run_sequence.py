@@ -85,9 +85,11 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     cuda = dev.type == "cuda"
     engines = [engine_cls(renderer.K, opts, renderer.W, renderer.H, batch=bounds[g + 1] - bounds[g], device=dev,
                           ncap=16384, pcap=16384, fcap=max_f + 8) for g in range(G)]
-    # group 0 on a high-priority stream: its bootstrap finishes first and its (latency-bound)
-    # steps then run while the later groups' bootstrap SIFT fills the GPU
-    prio = os.environ.get("VO_SEQ_PRIO", "1") == "1"
+    # every group on a normal-priority stream of its own.  VO_SEQ_PRIO=1 puts group 0 on a
+    # high-priority stream (its bootstrap finishes first and its steps run while the later
+    # groups' SIFT fills the GPU): that helped with a device sync after the bootstraps, and costs
+    # ~12 % without one (64 shards: 26.1-26.4k vs 29.9k frames/s, profiles/r4_seq_prio.txt)
+    prio = os.environ.get("VO_SEQ_PRIO", "0") == "1"
     streams = [torch.cuda.Stream(dev, priority=-1 if (prio and g == 0) else 0) if cuda and G > 1 else None
                for g in range(G)]
 
