@@ -287,13 +287,13 @@ def c5_leg(device, chains=256, steps=6, warmup=2, groups=2):
 
 def seq_chains_for(world: int) -> int:
     """Shards per GPU of the whole-sequence job.  The wall time is bootstrap(B) + (SEQ_LEN /
-    (world B) + 27) x step(B): on one GPU 64 chains minimise it (measured
-    sweep, profiles/r4_seq_sweep.jsonl); with more GPUs each one's shards get shorter, the
-    27-step overlap/bootstrap tail stays, and the step latency falls with B down to the
-    single-chain floor, so B shrinks to keep world x B near 64 (16 per GPU at most 4x over).
-    Reference fixtures exist for every resulting cut (64 shards for 1, 2 and 4 GPUs, 128 for
-    8)."""
-    return max(16, 64 // max(1, world))
+    (world B) + 27) x step(B).  Measured on one GPU with two stream groups
+    (profiles/r4_seq_prio0_sweep.jsonl, r4_seq_small_sweep.jsonl): B = 64 gives 0.031 s +
+    98 x 1.24 ms, B = 32 0.018 s + 98 x 0.80 ms, B = 16 (one group) 0.013 s + 98 x 0.75 ms.  So
+    64 on one GPU, and 32 per GPU beyond (64, 128, 256 shards on 2, 4, 8 GPUs: ~0.097, 0.069,
+    0.054 s by the model, against 0.087 s and 0.060 s for 16 per GPU on 4 and 8).  Reference
+    fixtures exist for every resulting cut."""
+    return 64 if world <= 1 else 32
 
 
 def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=2):
