@@ -59,9 +59,11 @@ struct PyrLevelArgs {
 };
 
 // L0: level 0 (frame bytes; its instantiation carries no source-staging LDS, so more blocks
-// fit per CU)
-template <bool L0, int TH>
-__global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
+// fit per CU).  FSRC (pyrDown levels): the source level is level 0 read straight from the frame
+// at reflect-101 coordinates -- the values level 0's materialised border holds -- so level 1
+// needs no level-0 tile of another block (k_pyr01 builds both in one launch).
+template <bool L0, int TH, bool FSRC>
+VO_DEV void pyr_tile(const PyrLevelArgs& A, int px0, int py0)
 {
     constexpr int PH = TH + 2, SH = 2 * PH + 3, RPT = TH / 8;   // tile rows + halo, staged source rows, rows / thread
     __shared__ uint32_t PVw[PH * PV_W / 4];
@@ -70,7 +72,6 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
     uint8_t* PV = (uint8_t*)PVw;
     const int tid = threadIdx.x;
     const int b = blockIdx.z;
-    const int px0 = blockIdx.x * PT_W, py0 = blockIdx.y * TH;
     const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
     // level coordinates of the tile's rows / cols (-1: outside the padded level)
     if (tid < 4) mm[tid] = (tid & 1) ? -1 : 0x7fffffff;
@@ -120,15 +121,31 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         const int gx0 = sx0 + VO_BORDER;                 // padded source column of sx0
         const int ax0 = gx0 & ~3, sh = gx0 - ax0;
         const int nwd = (sx1 + VO_BORDER - ax0) / 4 + 1; // dwords per staged row
-        const uint8_t* sbase = A.src + (int64_t)b * A.sstride + A.soff + ax0;
         constexpr int NSR = (SH * (PS_W / 4) + 255) / 256;
         uint32_t v[NSR];
+        if constexpr (FSRC) {
+            // staged byte j of row r = level-0 padded column ax0 + j = frame column
+            // refl101(ax0 + j - VO_BORDER), frame row refl101(sy0 + r)
+            const uint8_t* fr = A.src + (int64_t)b * A.sstride;
 #pragma unroll
-        for (int i = 0; i < NSR; ++i) {
-            const int e = tid + 256 * i;
-            const int r = e / (PS_W / 4), c = e - r * (PS_W / 4);
-            const bool in = r < nsr && c < nwd;
-            v[i] = *(const uint32_t*)(sbase + (int64_t)(sy0 + (in ? r : 0) + VO_BORDER) * A.spitch + 4 * (in ? c : 0));
+            for (int i = 0; i < NSR; ++i) {
+                const int e = tid + 256 * i;
+                const int r = e / (PS_W / 4), c = e - r * (PS_W / 4);
+                const bool in = r < nsr && c < nwd;
+                const uint8_t* row = fr + (int64_t)refl101(sy0 + (in ? r : 0), A.sh) * A.sw;
+                const int cb = ax0 - VO_BORDER + 4 * (in ? c : 0);
+                v[i] = (uint32_t)row[refl101(cb, A.sw)] | ((uint32_t)row[refl101(cb + 1, A.sw)] << 8) |
+                       ((uint32_t)row[refl101(cb + 2, A.sw)] << 16) | ((uint32_t)row[refl101(cb + 3, A.sw)] << 24);
+            }
+        } else {
+            const uint8_t* sbase = A.src + (int64_t)b * A.sstride + A.soff + ax0;
+#pragma unroll
+            for (int i = 0; i < NSR; ++i) {
+                const int e = tid + 256 * i;
+                const int r = e / (PS_W / 4), c = e - r * (PS_W / 4);
+                const bool in = r < nsr && c < nwd;
+                v[i] = *(const uint32_t*)(sbase + (int64_t)(sy0 + (in ? r : 0) + VO_BORDER) * A.spitch + 4 * (in ? c : 0));
+            }
         }
 #pragma unroll
         for (int i = 0; i < NSR; ++i) {
@@ -234,6 +251,24 @@ __global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
         }
         int16_t* dq = A.der + (int64_t)b * A.dstride + 2 * (A.off + (int64_t)py * A.pitch + px);
         *(uint4*)dq = make_uint4(o[0], o[1], o[2], o[3]);          // (dx, dy) of 4 pixels, 16 B
+    }
+}
+
+template <bool L0, int TH>
+__global__ void __launch_bounds__(256) k_pyr_level(PyrLevelArgs A)
+{
+    pyr_tile<L0, TH, false>(A, blockIdx.x * PT_W, blockIdx.y * TH);
+}
+
+// Levels 0 and 1 in one launch (few chains, where a launch is mostly latency): blocks with
+// blockIdx.y < ty0 take level-0 tiles, the others level-1 tiles computed from the frame
+// (pyr_tile FSRC); both grids' columns are covered by gridDim.x, surplus blocks exit.
+__global__ void __launch_bounds__(256) k_pyr01(PyrLevelArgs A0, PyrLevelArgs A1, int tx0, int ty0, int tx1)
+{
+    if ((int)blockIdx.y < ty0) {
+        if ((int)blockIdx.x < tx0) pyr_tile<true, PYR0_TH, false>(A0, blockIdx.x * PT_W, blockIdx.y * PYR0_TH);
+    } else if ((int)blockIdx.x < tx1) {
+        pyr_tile<false, PT_H, true>(A1, blockIdx.x * PT_W, (blockIdx.y - ty0) * PT_H);
     }
 }
 
@@ -1919,7 +1954,33 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
                             int64_t frame_stride, vo_stream_t stream)
 {
     if (!d || !s || !frames || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
-    for (int l = 0; l < d->nlev; ++l) {
+    // very few chains (the drop-in class's one): levels 0 and 1 in one launch (k_pyr01; one chain
+    // 1,992-2,015 -> 2,029-2,049 frames/s eager).  At 32 chains per launch (the sequence job) the
+    // fused kernel's 30 KB of LDS and byte-wise frame staging cost more than the launch saves
+    // (29.4k -> 29.0k frames/s).  VO_PYR01=0 / 1 forces it off / on.
+    static const int p01_env = [] { const char* e = getenv("VO_PYR01"); return e ? atoi(e) : -1; }();
+    const bool fuse01 = d->nlev >= 2 && (p01_env >= 0 ? p01_env == 1 : d->B <= 8);
+    if (fuse01) {
+        PyrLevelArgs A0, A1;
+        A0.src = frames; A0.sstride = frame_stride; A0.sw = A0.sh = A0.spitch = 0; A0.soff = 0;
+        A1.src = frames; A1.sstride = frame_stride; A1.sw = d->lvl_w[0]; A1.sh = d->lvl_h[0]; A1.spitch = 0; A1.soff = 0;
+        PyrLevelArgs* As[2] = {&A0, &A1};
+        for (int l = 0; l < 2; ++l) {
+            PyrLevelArgs& A = *As[l];
+            A.pyr = s->pyr[cur]; A.pstride = d->pyr_stride;
+            A.der = s->der[cur]; A.dstride = d->der_stride;
+            A.w = d->lvl_w[l]; A.h = d->lvl_h[l]; A.pitch = d->lvl_pitch[l]; A.off = d->lvl_off[l];
+            A.level = l;
+            if (A.pitch % 64 || A.pitch < A.w + 2 * VO_BORDER) return VO_EARG;
+        }
+        const int pw0 = A0.w + 2 * VO_BORDER, ph0 = A0.h + 2 * VO_BORDER;
+        const int pw1 = A1.w + 2 * VO_BORDER, ph1 = A1.h + 2 * VO_BORDER;
+        const int tx0 = (pw0 + PT_W - 1) / PT_W, ty0 = (ph0 + PYR0_TH - 1) / PYR0_TH;
+        const int tx1 = (pw1 + PT_W - 1) / PT_W, ty1 = (ph1 + PT_H - 1) / PT_H;
+        dim3 g(tx0 > tx1 ? tx0 : tx1, ty0 + ty1, d->B);
+        hipLaunchKernelGGL(k_pyr01, g, dim3(256), 0, VO_STREAM(stream), A0, A1, tx0, ty0, tx1);
+    }
+    for (int l = fuse01 ? 2 : 0; l < d->nlev; ++l) {
         PyrLevelArgs A;
         if (l == 0) {
             A.src = frames; A.sstride = frame_stride; A.sw = A.sh = A.spitch = 0; A.soff = 0;
