@@ -143,6 +143,9 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
             with on(g):
                 eng.reserve_bootstrap()
     _sync(dev)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()                     # every rank starts its clock together (max-over-ranks wall)
     # without time_boot the groups are not synchronised after their bootstraps (a group steps
     # as soon as its own bootstrap is done); the bootstrap time is then the latest group's
     # end-of-bootstrap event
