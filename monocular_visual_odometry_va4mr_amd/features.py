@@ -108,10 +108,15 @@ def _scratch(dev, nbytes: int) -> torch.Tensor:
     when the groups' bootstraps overlapped more: half the shards of one group differed from the
     reference runs)."""
     key = (dev, torch.cuda.current_stream(dev).cuda_stream)
-    buf = _SCRATCH.get(key)
+    buf = _SCRATCH.pop(key, None)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        _SCRATCH[key] = buf
+    _SCRATCH[key] = buf                    # most recently used last
+    # streams come and go (every sequence run makes its own): keep the 8 most recent buffers.
+    # A dropped buffer was allocated on its own stream, so the caching allocator hands its
+    # memory only to later work of that stream, after the work already queued there.
+    while len(_SCRATCH) > 8:
+        _SCRATCH.pop(next(iter(_SCRATCH)))
     return buf
 
 
