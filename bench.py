@@ -83,8 +83,12 @@ def parse():
                     help="shards per GPU of the whole-sequence job (n_shards = world x this; default "
                          "seq_chains_for(world))")
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
-    ap.add_argument("--hw-queues", type=int, default=None,
-                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; <= 32)")
+    # 8 hardware queues per process (HIP's default is 4): the legs' stream groups then no longer
+    # share queues by accident of the process's stream history -- the sequence leg kept 29.6-29.7k
+    # frames/s after a captured one-chain step instead of dropping to 25.8k; every leg measured
+    # equal or slightly faster (profiles/r4_hw_queues.txt).  0 leaves the environment's value.
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; <= 32; 0 = leave)")
     return ap.parse_args()
 
 
