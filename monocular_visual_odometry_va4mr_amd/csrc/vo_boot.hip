@@ -188,7 +188,10 @@ VO_DEV int solve_poly(const double* c_in, int n0, Cplx* roots)
     return n;
 }
 
-VO_DEV int five_point(const double* q1, const double* q2, double* E10)
+// five_point in three parts: the Groebner-basis coefficients of the degree-10 polynomial in z
+// (false if the 10x10 elimination is singular), the roots, and each real root's essential matrix.
+VO_DEV bool five_point_coeffs(const double* q1, const double* q2, double (&basis)[4][9], double (&b)[3][13],
+                              double (&coeffs)[11])
 {
     double Qt[9 * 5];
     for (int i = 0; i < 5; ++i) {
@@ -215,7 +218,6 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
             for (int i = k; i < 9; ++i) Qt[i * 5 + j] -= s * H[k][i];
         }
     }
-    double basis[4][9];
     for (int b = 0; b < 4; ++b) {
         double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         v[5 + b] = 1.0;
@@ -289,8 +291,7 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
                 for (int c = 0; c < 20; ++c) { if (c < 10) A[r * 10 + c] = acc.c[c]; else Bm[r * 10 + (c - 10)] = acc.c[c]; }
             }
     }
-    if (!gauss_solve(A, 10, Bm, 10)) return 0;
-    double b[3][13];
+    if (!gauss_solve(A, 10, Bm, 10)) return false;
     for (int i = 0; i < 3; ++i) {
         const double* g1 = Bm + (4 + 2 * i) * 10;
         const double* g2 = Bm + (5 + 2 * i) * 10;
@@ -310,7 +311,6 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
         for (int k = 0; k < 4; ++k) { P[i][0][3 - k] = b[i][k]; P[i][1][3 - k] = b[i][4 + k]; }
         for (int k = 0; k < 5; ++k) P[i][2][4 - k] = b[i][8 + k];
     }
-    double coeffs[11];
     for (int k = 0; k < 11; ++k) coeffs[k] = 0;
     {
         const int perm[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
@@ -326,12 +326,15 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
             for (int k = 0; k < 11; ++k) coeffs[k] += psign[s] * t2[k];
         }
     }
-    Cplx roots[10];
-    const int nroots = solve_poly(coeffs, 10, roots);
-    int count = 0;
-    for (int i = 0; i < nroots; ++i) {
-        if (fabs(roots[i].im) > 1e-10) continue;
-        double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+    return true;
+}
+
+// the essential matrix of one root (false: complex, or no finite (x, y)), normalised
+VO_DEV bool five_point_root_E(const Cplx root, const double (&basis)[4][9], const double (&b)[3][13], double* E)
+{
+    {
+        if (fabs(root.im) > 1e-10) return false;
+        double z1 = root.re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
         double Bz[9];
         for (int j = 0; j < 3; ++j) {
             const double* br = b[j];
@@ -343,7 +346,7 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
         for (int q = 0; q < 9; ++q) Aw[q] = Bz[q];
         svd_jacobi<3, 3>(Aw, w, V);
         double xy1[3] = {V[2], V[5], V[8]};
-        if (fabs(xy1[2]) < 1e-10) continue;
+        if (fabs(xy1[2]) < 1e-10) return false;
         double x = xy1[0] / xy1[2], y = xy1[1] / xy1[2];
         double ev[9], nrm = 0;
         for (int e = 0; e < 9; ++e) {
@@ -351,10 +354,93 @@ VO_DEV int five_point(const double* q1, const double* q2, double* E10)
             nrm += ev[e] * ev[e];
         }
         nrm = sqrt(nrm);
-        for (int e = 0; e < 9; ++e) E10[count * 9 + e] = ev[e] / nrm;
-        ++count;
+        for (int e = 0; e < 9; ++e) E[e] = ev[e] / nrm;
     }
+    return true;
+}
+
+VO_DEV int five_point(const double* q1, const double* q2, double* E10)
+{
+    double basis[4][9], b[3][13], coeffs[11];
+    if (!five_point_coeffs(q1, q2, basis, b, coeffs)) return 0;
+    Cplx roots[10];
+    const int nroots = solve_poly(coeffs, 10, roots);
+    int count = 0;
+    for (int i = 0; i < nroots; ++i)
+        if (five_point_root_E(roots[i], basis, b, E10 + count * 9)) ++count;
     return count;
+}
+
+// five_point for one hypothesis on 10 lanes (li = 0..9 of a group starting at lane gb): the
+// coefficients on every lane, then the degree-10 Weierstrass sweeps with lane li owning root li,
+// pipelined (root t's update needs the new roots 0..t-1 only in its denominator, whose factors
+// are multiplied in j order: lane i takes factor t (new root t) at step t < i and its old-root
+// factors t+1..9 at step i; its numerator, which depends on its own root only, at the sweep's
+// start), then each real root's essential matrix on its lane, written in root order.  The same
+// operations in the same order as five_point, so the same models.  Other degrees: lane 0 runs
+// five_point.
+VO_DEV int five_point_grp(const double* q1, const double* q2, double* E10, int li, int gb)
+{
+    double basis[4][9], b[3][13], coeffs[11];
+    if (!five_point_coeffs(q1, q2, basis, b, coeffs)) return 0;
+    if (!(fabs(coeffs[10]) + fabs(0.0) > DBL_EPSILON)) {
+        int nm = 0;
+        if (li == 0) nm = five_point(q1, q2, E10);
+        return __shfl(nm, gb, 64);
+    }
+    Cplx co[11], r[10];
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) { co[i].re = coeffs[i]; co[i].im = 0; }
+    {
+        Cplx p = {1, 0}, rr = {1, 1};
+#pragma unroll
+        for (int i = 0; i < 10; ++i) { r[i] = p; p = c_mul(p, rr); }
+    }
+    for (int iter = 0; iter < 300; ++iter) {
+        Cplx pm = r[0];
+#pragma unroll
+        for (int i = 1; i < 10; ++i) if (li == i) pm = r[i];
+        Cplx num = co[10], den = co[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) num = c_add(c_mul(num, pm), co[10 - j - 1]);
+        double maxDiff = 0;
+#pragma unroll
+        for (int t = 0; t < 10; ++t) {
+            Cplx nr = {0, 0};
+            double a = 0;
+            if (li == t) {
+#pragma unroll
+                for (int j = t + 1; j < 10; ++j) {
+                    Cplx d = c_sub(pm, r[j]);
+                    if (!(d.re == 0 && d.im == 0)) den = c_mul(den, d);
+                }
+                const Cplx q = c_div(num, den);
+                nr = c_sub(pm, q);
+                a = sqrt(q.re * q.re + q.im * q.im);
+            }
+            r[t].re = __shfl(nr.re, gb + t, 64);
+            r[t].im = __shfl(nr.im, gb + t, 64);
+            a = __shfl(a, gb + t, 64);
+            if (a > maxDiff) maxDiff = a;
+            if (li > t) {
+                Cplx d = c_sub(pm, r[t]);
+                if (!(d.re == 0 && d.im == 0)) den = c_mul(den, d);
+            }
+        }
+        if (maxDiff <= 0) break;
+    }
+    Cplx mine = r[0];
+#pragma unroll
+    for (int i = 1; i < 10; ++i) if (li == i) mine = r[i];
+    if (fabs(mine.im) < 1e-100) mine.im = 0;
+    double E[9];
+    const bool ok = five_point_root_E(mine, basis, b, E);
+    const uint64_t m = (__ballot(ok) >> gb) & 0x3FFull;
+    if (ok) {
+        const int slot = __popcll(m & ((1ull << li) - 1ull));
+        for (int e = 0; e < 9; ++e) E10[slot * 9 + e] = E[e];
+    }
+    return __popcll(m);
 }
 
 // ------------------------------------------------------------------ E-RANSAC
@@ -426,11 +512,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
     uint64_t rng = ~0ULL;
     if (tid == 0) { sh[0] = 0; sh[1] = A.max_iters > 1 ? A.max_iters : 1; sh[2] = 0; }
     __syncthreads();
+    // one block per CU (WPE 1): each hypothesis on 10 lanes (five_point_grp), 6 per wave, 24 per
+    // round; more chains than CUs (WPE 2): one hypothesis per lane of wave 0, 64 per round
+    constexpr int NH = WPE == 1 ? 24 : EHYP;
     while (true) {
         const int it0 = sh[0], niters0 = sh[1];
         if (it0 >= niters0) break;
         if (tid == 0) {
-            for (int h = 0; h < EHYP; ++h)
+            for (int h = 0; h < NH; ++h)
                 for (int i = 0; i < 5; ++i) {
                     for (;;) {
                         int v = (int)(rng_next(rng) % (uint32_t)n);
@@ -442,7 +531,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                 }
         }
         __syncthreads();
-        if (tid < EHYP) {
+        if constexpr (WPE == 1) {
+            const int lane = lane_id(), g = lane / 10, li = lane - 10 * g;
+            const int h = wave_id() * 6 + g;
+            if (lane < 60 && h < NH) {
+                int nm = 0;
+                if (it0 + h < niters0) {
+                    double s1[10], s2[10];
+                    for (int j = 0; j < 5; ++j) {
+                        const int id = sub[h][j];
+                        s1[2 * j] = q1[2 * id]; s1[2 * j + 1] = q1[2 * id + 1];
+                        s2[2 * j] = q2[2 * id]; s2[2 * j + 1] = q2[2 * id + 1];
+                    }
+                    nm = five_point_grp(s1, s2, models + 90 * h, li, 10 * g);
+                }
+                if (li == 0) nmod[h] = nm;
+            }
+        } else if (tid < EHYP) {
             const int h = tid;
             int nm = 0;
             if (it0 + h < niters0) {
@@ -459,10 +564,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         __syncthreads();
         {
             const int w = wave_id(), lane = lane_id(), nw = blockDim.x >> 6;
-            for (int h0 = 0; h0 < EHYP; h0 += nw) {
+            for (int h0 = 0; h0 < NH; h0 += nw) {
                 if (it0 + h0 >= sh[1]) break;                                 // block-uniform
                 const int h = h0 + w;
-                if (h < EHYP)
+                if (h < NH)
                     for (int m = 0; m < nmod[h]; ++m) {
                         const double* Em = models + 90 * h + 9 * m;
                         int c = 0;
@@ -474,7 +579,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                 __syncthreads();
                 if (tid == 0) {
                     int niters = sh[1], best = sh[2];
-                    const int h1 = h0 + nw < EHYP ? h0 + nw : EHYP;
+                    const int h1 = h0 + nw < NH ? h0 + nw : NH;
                     for (int hh = h0; hh < h1; ++hh) {
                         if (it0 + hh >= niters) break;
                         for (int m = 0; m < nmod[hh]; ++m) {
@@ -492,7 +597,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                 __syncthreads();
             }
         }
-        if (tid == 0) sh[0] = it0 + EHYP;
+        if (tid == 0) sh[0] = it0 + NH;
         __syncthreads();
     }
     const bool ok = sh[2] > 0;

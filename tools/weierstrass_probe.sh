@@ -5,6 +5,9 @@
 #   bash tools/weierstrass_probe.sh            synthetic matches (20 problems, 30 % outliers)
 #   bash tools/weierstrass_probe.sh real       the C2 bootstrap matches of 6 shard starts
 #                                              (tools/dump_boot_matches.py, oracle pipeline)
+#   bash tools/weierstrass_probe.sh pipe       k_essential's 10-lane pipelined sweep schedule
+#                                              (five_point_grp), emulated on the CPU, against
+#                                              the oracle's serial solve_poly, bit for bit
 set -e
 mkdir -p /tmp/wk
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -12,6 +15,13 @@ sed 's|int nroots = solve_poly(coeffs, 10, roots);|int nroots = solve_poly(coeff
 cp "$R/tools/micro/weierstrass_probe.c" /tmp/wk/
 gcc -O2 -ffp-contract=off -fno-fast-math -std=gnu11 -I"$R/oracle" -I"$R/monocular_visual_odometry_va4mr_amd/csrc" \
     /tmp/wk/weierstrass_probe.c "$R/oracle/vo_oracle_img.c" -o /tmp/wk/probe -lm
+if [ "$1" = pipe ]; then
+  cp "$R/tools/micro/weierstrass_pipe_check.c" /tmp/wk/
+  gcc -O2 -ffp-contract=off -fno-fast-math -std=gnu11 -I"$R/oracle" -I"$R/monocular_visual_odometry_va4mr_amd/csrc" \
+      -I/tmp/wk /tmp/wk/weierstrass_pipe_check.c "$R/oracle/vo_oracle_img.c" -o /tmp/wk/pipe_check -lm
+  /tmp/wk/pipe_check
+  exit 0
+fi
 if [ "$1" = real ]; then
   python3 "$R/tools/dump_boot_matches.py" 0 700 1400 2100 2800 3500
   python3 -c "
