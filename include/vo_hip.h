@@ -126,6 +126,12 @@ typedef struct vo_state {
 const char* vo_version(void);
 int vo_device_arch(char* buf, int len);          /* gcnArchName of the current device */
 int vo_device_cus(void);                          /* compute units of the current device (or < 0) */
+/* Launch-shape threshold: several entry points pick their kernel form by comparing the chain
+ * count B with the device's compute units (vo_essential / vo_bootstrap / vo_triangulate /
+ * vo_pnp / vo_pnp_triangulate: one block per chain at or above the CU count, split or
+ * unconstrained forms below).  n > 0 makes those decisions assume n CUs (test hook: every form
+ * on a small batch); n = 0 restores the device's own count.  Results never depend on it. */
+int vo_set_launch_cus(int n);
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 
@@ -255,17 +261,11 @@ int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, int64_t img
 int vo_sift_retain_best_rows(float* kp_out, int32_t n, int32_t nfeatures, int32_t* counters, int32_t* scratch,
                              float* tmp, vo_stream_t stream);
 
-/* BFMatcher().knnMatch(q, t, k=2) (:36,229) for integer-valued float descriptors of
- * dim 128: bf16 MFMA distance tiles (exact), top-2 per query with OpenCV's tie order.
- * nq/nt are read on the device; idx2 [qcap][2] (-1 if absent), dist2 [qcap][2]. */
-int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt,
-               int32_t qcap, int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream);
-
 /* Batched BFMatcher().knnMatch(q, t, k=2) (:36,229) for B independent problems on MFMA
  * (csrc/vo_match.hip): q [B][qcap][128], t [B][tcap][128] integer-valued float descriptors
  * (SIFT: 0..255), device counts nq[B] / nt[B]; idx2 [B][qcap][2] (-1 if absent), dist2
  * [B][qcap][2] (FLT_MAX if absent); rows >= nq[b] untouched.  Same (distance, index) order and
- * float distances as vo_bf_knn2 / OpenCV.  scratch: device bytes >= vo_bf_knn2_batch_scratch(). */
+ * float distances as OpenCV (batchDistance + the k = 2 insertion).  scratch: device bytes >= vo_bf_knn2_batch_scratch(). */
 int64_t vo_bf_knn2_batch_scratch(int B, int32_t qcap, int32_t tcap);
 int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_t qcap, const float* t,
                      const int32_t* nt, int32_t tcap, int32_t dim, int32_t* idx2, float* dist2,

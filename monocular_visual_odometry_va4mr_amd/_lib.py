@@ -128,6 +128,7 @@ def _declare(L):
         "vo_version": ([], C.c_char_p),
         "vo_device_arch": ([C.c_char_p, C.c_int], C.c_int),
         "vo_device_cus": ([], C.c_int),
+        "vo_set_launch_cus": ([C.c_int], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),
@@ -151,7 +152,6 @@ def _declare(L):
         "vo_sift": ([SB, P, C.c_int, C.c_int, P], C.c_int),
         "vo_sift_batch": ([SB, C.c_int, P, C.c_int64, C.c_int, C.c_int, P], C.c_int),
         "vo_sift_retain_best_rows": ([P, i32, i32, P, P, P, P], C.c_int),
-        "vo_bf_knn2": ([P, P, P, P, i32, i32, P, P, P], C.c_int),
         "vo_ratio_matches": ([C.c_int, P, P, i32, P, P, P, i32, f64, P, P, P, i32, P], C.c_int),
         "vo_find_essential": ([O, C.c_int, P, P, P, i32, f64, f64, i32, P, P, P, P, i32, P], C.c_int),
         "vo_recover_pose": ([O, C.c_int, P, P, P, P, i32, P, P, P, P, P], C.c_int),

@@ -13,6 +13,16 @@ extern "C" int vo_device_cus(void)
     return n;
 }
 
+// launch-shape threshold override (vo_set_launch_cus; read by device_cus() in vo_dev.h)
+int vo_launch_cus_override = 0;
+
+extern "C" int vo_set_launch_cus(int n)
+{
+    if (n < 0) return VO_EARG;
+    vo_launch_cus_override = n;
+    return VO_OK;
+}
+
 extern "C" int vo_device_arch(char* buf, int len)
 {
     if (!buf || len <= 0) return VO_EARG;

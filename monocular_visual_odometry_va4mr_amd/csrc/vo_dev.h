@@ -204,9 +204,12 @@ VO_DEV uint32_t rng_next(uint64_t& s)
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
 // host: compute units of the current device, cached per device id (launch-shape decisions of
-// the C ABI entry points; a benign race only stores the same value twice)
+// the C ABI entry points; a benign race only stores the same value twice), or the count set by
+// vo_set_launch_cus (test hook: the many-chains forms on a small batch)
+extern int vo_launch_cus_override;
 static inline int device_cus()
 {
+    if (vo_launch_cus_override > 0) return vo_launch_cus_override;
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
     static int cache[64] = {0};

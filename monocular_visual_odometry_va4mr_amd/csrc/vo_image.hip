@@ -890,11 +890,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // per sum (exact: |dI| <= 4080, weights <= 2^14)
                 const v2i16 wp0 = as_v2i16((uint32_t)(iw00 & 0xffff) | ((uint32_t)iw01 << 16));
                 const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
+#ifdef VO_LK_TENSOR_BATCH
+                // diagnostics build (the round-4 variant that was dropped): the
+                // level's 24 tensor LDS reads issued together ahead of a scheduling barrier
+                uint32_t tdq[MAXJ][4];
+                int tsv[MAXJ][4];
+#pragma unroll
+                for (int j = 0; j < MAXJ; ++j) {
+                    const uint8_t* s = ir8 + toff[j] + ish;
+                    const uint32_t* d = DR + toff[j];
+                    tdq[j][0] = d[0]; tdq[j][1] = d[1]; tdq[j][2] = d[QS]; tdq[j][3] = d[QS + 1];
+                    tsv[j][0] = s[0]; tsv[j][1] = s[1]; tsv[j][2] = s[QS]; tsv[j][3] = s[QS + 1];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
 #ifdef VO_LKX_NOTENSOR
                     const uint32_t d00 = (uint32_t)(toff[j] * 977) & 0x03ff03ffu, d01 = d00 + 3, d10 = d00 + 5, d11 = d00 + 9;
                     const int v = (toff[j] * 31) & 8191;
+#elif defined(VO_LK_TENSOR_BATCH)
+                    const uint32_t d00 = tdq[j][0], d01 = tdq[j][1], d10 = tdq[j][2], d11 = tdq[j][3];
+                    const int v = DESCALE(__mul24(tsv[j][0], iw00) + __mul24(tsv[j][1], iw01) +
+                                          __mul24(tsv[j][2], iw10) + __mul24(tsv[j][3], iw11), 9);
 #else
                     const uint8_t* s = ir8 + toff[j] + ish;
                     const uint32_t* d = DR + toff[j];
@@ -2069,17 +2087,16 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     const bool staged15 = P.win_w == 15 && P.win_h == 15 && P.pstride >= pyr_end + 64;
     const size_t lds = 4 * (size_t)(P.win_w + 2 * LK_M) * (P.win_h + 2 * LK_M);
     if (lds > 60 * 1024) return VO_EARG;
-    // Fused levels (one launch, each wave carries its point from the coarsest level to level
-    // 0 in registers) unless VO_LK_FUSED=0: a level's launch lasts as long as its slowest
-    // point (up to max_count iterations), so separate launches pay that tail once per level.
-    static const int fused_env = [] { const char* e = getenv("VO_LK_FUSED"); return e ? atoi(e) : 1; }();
-    if (staged15 && fused_env) {
+    // 15x15 (every reference configuration, main.py:36,66,96): all levels in one launch, each
+    // wave carrying its point from the coarsest level to level 0 in registers.  Other window
+    // sizes (cv2.calcOpticalFlowPyrLK's default 21x21 on the cv2compat surface): k_lk, one
+    // launch per level.
+    if (staged15) {
         hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {
-        if (staged15) hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, level, level, B, nb, xcd_env);
-        else if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
+        if (npx <= 256) hipLaunchKernelGGL(k_lk<4>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
         else hipLaunchKernelGGL(k_lk<16>, dim3(nblk), dim3(64), lds, st, P, level, B, nb);
     }
     return hip_ok() ? VO_OK : VO_EHIP;

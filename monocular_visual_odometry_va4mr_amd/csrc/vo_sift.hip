@@ -350,47 +350,6 @@ __global__ void k_nn_down(const float* __restrict__ src, int sw, int sh, float* 
     dst[(int64_t)y * dw + x] = src[(int64_t)sy * sw + sx];
 }
 
-__global__ void k_extrema(vo_sift_buf sb, int o, int layer)
-{
-    const SiftImg im = sift_img(sb, blockIdx.z);
-    const int w = sb.oct_w[o], h = sb.oct_h[o];
-    const int c = blockIdx.x * blockDim.x + threadIdx.x + SIFT_IMG_BORDER;
-    const int r = blockIdx.y + SIFT_IMG_BORDER;
-    bool ext = c < w - SIFT_IMG_BORDER && r < h - SIFT_IMG_BORDER;
-    if (ext) {
-        const int idx = o * (N_LAYERS + 2) + layer;
-        const float* img = im.dog + sb.dog_off[idx];
-        const float* prev = im.dog + sb.dog_off[idx - 1];
-        const float* next = im.dog + sb.dog_off[idx + 1];
-        const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
-        const float val = img[(int64_t)r * w + c];
-        ext = fabsf(val) > threshold;
-        for (int dz = 0; dz < 3 && ext; ++dz) {
-            const float* L = dz == 0 ? prev : (dz == 1 ? img : next);
-            for (int dy = -1; dy <= 1 && ext; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    const float u = L[(int64_t)(r + dy) * w + (c + dx)];
-                    if (val > 0 ? !(val >= u) : !(val <= u)) { ext = false; break; }
-                }
-        }
-    }
-    // one atomic per wave: the list order is irrelevant (keypoints are canonically sorted)
-    const uint64_t m = __ballot(ext);
-    if (m == 0) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&im.counters[0], __popcll(m));
-    base = __shfl(base, leader, 64);
-    if (!ext) return;
-    const int k = base + __popcll(m & ((1ull << lane) - 1ull));
-    if (k < sb.cand_cap) {
-        im.cand[4 * k] = o; im.cand[4 * k + 1] = layer; im.cand[4 * k + 2] = r; im.cand[4 * k + 3] = c;
-    } else {
-        im.counters[3] = 1;
-    }
-}
-
 // All three extremum layers of one octave from one LDS tile: 64 x 16 interior pixels per
 // block, the five DoG layers of the octave with a 1-pixel halo staged once; each pixel that
 // passes the threshold is compared with the max / min of its 3x3x3 neighbourhood (separable:
@@ -608,82 +567,7 @@ VO_DEV bool adjust_local_extrema(const vo_sift_buf& sb, const float* dogs, KP& k
     return true;
 }
 
-VO_DEV float orientation_hist(const float* img, int w, int h, int px, int py, int radius, float sigma, float* hist,
-                              const float* tab)
-{
-    const int n = SIFT_ORI_HIST_BINS;
-    float expf_scale = -1.f / (2.f * sigma * sigma);
-    float th[SIFT_ORI_HIST_BINS + 4];
-    float* temphist = th + 2;
-    for (int i = 0; i < n; ++i) temphist[i] = 0.f;
-    for (int i = -radius; i <= radius; ++i) {
-        int y = py + i;
-        if (y <= 0 || y >= h - 1) continue;
-        for (int j = -radius; j <= radius; ++j) {
-            int x = px + j;
-            if (x <= 0 || x >= w - 1) continue;
-            float dx = DAT(img, w, y, x + 1) - DAT(img, w, y, x - 1);
-            float dy = DAT(img, w, y - 1, x) - DAT(img, w, y + 1, x);
-            float wt = exp32f((float)(i * i + j * j) * expf_scale, tab);
-            float ori = fast_atan2(dy, dx);
-            float mag = sqrtf(dx * dx + dy * dy);
-            int bin = __float2int_rn((n / 360.f) * ori);
-            if (bin >= n) bin -= n;
-            if (bin < 0) bin += n;
-            temphist[bin] += wt * mag;
-        }
-    }
-    temphist[-1] = temphist[n - 1];
-    temphist[-2] = temphist[n - 2];
-    temphist[n] = temphist[0];
-    temphist[n + 1] = temphist[1];
-    for (int i = 0; i < n; ++i)
-        hist[i] = (temphist[i - 2] + temphist[i + 2]) * (1.f / 16.f) + (temphist[i - 1] + temphist[i + 1]) * (4.f / 16.f) +
-                  temphist[i] * (6.f / 16.f);
-    float maxval = hist[0];
-    for (int i = 1; i < n; ++i) maxval = maxval > hist[i] ? maxval : hist[i];
-    return maxval;
-}
-
-__global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
-{
-    const SiftImg im = sift_img(sb, blockIdx.z);
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    const int nc = min(im.counters[0], sb.cand_cap);
-    if (k >= nc) return;
-    const float* tab = sb.consts + EXPTAB_OFF;
-    const int o = im.cand[4 * k], i0 = im.cand[4 * k + 1];
-    int r1 = im.cand[4 * k + 2], c1 = im.cand[4 * k + 3], layer = i0;
-    KP kpt;
-    if (!adjust_local_extrema(sb, im.dog, kpt, o, layer, r1, c1, 1.6f)) return;
-    const float scl_octv = kpt.size * 0.5f / (float)(1 << o);
-    float hist[SIFT_ORI_HIST_BINS];
-    const float* g = im.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
-    const float omax = orientation_hist(g, sb.oct_w[o], sb.oct_h[o], c1, r1, __float2int_rn(SIFT_ORI_RADIUS * scl_octv),
-                                        SIFT_ORI_SIG_FCTR * scl_octv, hist, tab);
-    const float mag_thr = (float)(omax * SIFT_ORI_PEAK_RATIO);
-    const int n = SIFT_ORI_HIST_BINS;
-    for (int j = 0; j < n; ++j) {
-        const int l = j > 0 ? j - 1 : n - 1;
-        const int r2 = j < n - 1 ? j + 1 : 0;
-        if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
-            float bin = j + 0.5f * (hist[l] - hist[r2]) / (hist[l] - 2 * hist[j] + hist[r2]);
-            bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
-            float angle = 360.f - (float)((360.f / n) * bin);
-            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-            const int q = atomicAdd(&im.counters[1], 1);
-            if (q < sb.kp_cap) {
-                float* out = im.kp + 8 * (int64_t)q;
-                out[0] = kpt.x; out[1] = kpt.y; out[2] = kpt.size; out[3] = angle; out[4] = kpt.response;
-                out[5] = __int_as_float(kpt.octave); out[6] = 0.f; out[7] = 0.f;
-            } else {
-                im.counters[3] = 1;
-            }
-        }
-    }
-}
-
-// Two-stage form of k_sift_kp (default; VO_SIFT_KP_SERIAL=1 selects k_sift_kp):
+// Keypoint refinement and orientation in two stages:
 //  k_sift_refine  adjustLocalExtrema per candidate (one thread each) -> refined records in
 //                 the hist scratch (12 floats each), count in counters[4];
 //  k_sift_ori     calcOrientationHist + peak interpolation with one WAVE per refined keypoint:
@@ -691,7 +575,6 @@ __global__ void __launch_bounds__(128) k_sift_kp(vo_sift_buf sb)
 //                 order), the 36 bins are owned by lanes 0..35 and each lane adds, in pixel order,
 //                 the values that land in its bin -- the serial accumulation order, so the
 //                 histogram, its smoothing, the peaks and the emitted keypoints are identical.
-//                 (k_sift_kp's temphist[36] is indexed dynamically, i.e. lives in scratch.)
 //                 Keypoints are appended with atomics; k_sift_sort_dedupe orders them.
 #define SIFT_REC 12
 __global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
@@ -1124,104 +1007,8 @@ __global__ void __launch_bounds__(RB_T) k_sift_retain_best(vo_sift_buf sb)
     if (tid == 0) im.counters[2] = kept;
 }
 
-__global__ void __launch_bounds__(64) k_sift_desc(vo_sift_buf sb)
-{
-    const SiftImg im = sift_img(sb, blockIdx.z);
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= im.counters[2]) return;
-    const float* tab = sb.consts + EXPTAB_OFF;
-    const float* kp = im.kp_out + 6 * (int64_t)q;
-    const int kpo = (int)kp[5];
-    int octave = kpo & 255, layer = (kpo >> 8) & 255;
-    octave = octave < 128 ? octave : (-128 | octave);
-    const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
-    const float size = kp[2] * scale;
-    const float ptx = kp[0] * scale, pty = kp[1] * scale;
-    const int oi = octave + 1;
-    const float* img = im.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
-    const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
-    float angle = 360.f - kp[3];
-    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-    const float ori = angle, scl = size * 0.5f;
-    const int d = 4, n = 8;
-    const int ptix = __float2int_rn(ptx), ptiy = __float2int_rn(pty);
-    float cos_t = (float)vcr_cos((double)(ori * (float)(M_PI / 180)));
-    float sin_t = (float)vcr_sin((double)(ori * (float)(M_PI / 180)));
-    const float bins_per_rad = n / 360.f;
-    const float exp_scale = -1.f / (d * d * 0.5f);
-    const float hist_width = SIFT_DESCR_SCL_FCTR * scl;
-    int radius = __float2int_rn(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
-    const int rmax = (int)sqrt(((double)cols) * cols + ((double)rows) * rows);
-    if (radius > rmax) radius = rmax;
-    cos_t /= hist_width;
-    sin_t /= hist_width;
-    float* hist = im.hist + 360 * (int64_t)q;
-    for (int i = 0; i < (d + 2) * (d + 2) * (n + 2); ++i) hist[i] = 0.f;
-    for (int i = -radius; i <= radius; ++i) {
-        for (int j = -radius; j <= radius; ++j) {
-            const float c_rot = j * cos_t - i * sin_t;
-            const float r_rot = j * sin_t + i * cos_t;
-            float rbin = r_rot + d / 2 - 0.5f;
-            float cbin = c_rot + d / 2 - 0.5f;
-            const int r = ptiy + i, c = ptix + j;
-            if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 && c > 0 && c < cols - 1))
-                continue;
-            const float dx = DAT(img, cols, r, c + 1) - DAT(img, cols, r, c - 1);
-            const float dy = DAT(img, cols, r - 1, c) - DAT(img, cols, r + 1, c);
-            const float wgt = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, tab);
-            const float o = fast_atan2(dy, dx);
-            const float mag = sqrtf(dx * dx + dy * dy) * wgt;
-            float obin = (o - ori) * bins_per_rad;
-            int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin), o0 = (int)floorf(obin);
-            rbin -= r0; cbin -= c0; obin -= o0;
-            if (o0 < 0) o0 += n;
-            if (o0 >= n) o0 -= n;
-            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-            const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-            const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-            const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-            const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-            const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-            const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-            const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-            hist[idx] += v_rco000;
-            hist[idx + 1] += v_rco001;
-            hist[idx + (n + 2)] += v_rco010;
-            hist[idx + (n + 3)] += v_rco011;
-            hist[idx + (d + 2) * (n + 2)] += v_rco100;
-            hist[idx + (d + 2) * (n + 2) + 1] += v_rco101;
-            hist[idx + (d + 3) * (n + 2)] += v_rco110;
-            hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
-        }
-    }
-    float* dst = im.desc + 128 * (int64_t)q;
-    for (int i = 0; i < d; ++i)
-        for (int j = 0; j < d; ++j) {
-            const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
-            hist[idx] += hist[idx + n];
-            hist[idx + 1] += hist[idx + n + 1];
-            for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = hist[idx + k];
-        }
-    const int len = d * d * n;
-    float nrm2 = 0;
-    for (int k = 0; k < len; ++k) nrm2 += dst[k] * dst[k];
-    const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
-    nrm2 = 0;
-    for (int i = 0; i < len; ++i) {
-        const float v = dst[i] < thr ? dst[i] : thr;
-        dst[i] = v;
-        nrm2 += v * v;
-    }
-    const float s = sqrtf(nrm2);
-    nrm2 = SIFT_INT_DESCR_FCTR / (s > FLT_EPSILON ? s : FLT_EPSILON);
-    for (int k = 0; k < len; ++k) {
-        const int iv = __float2int_rn(dst[k] * nrm2);
-        dst[k] = (float)(iv < 0 ? 0 : (iv > 255 ? 255 : iv));
-    }
-}
-
 // k_sift_desc_w: calcSIFTDescriptor with one WAVE per keypoint and the same arithmetic, in
-// the same order, as k_sift_desc (and the C restatement).
+// the same order, as the C restatement (oracle/vo_oracle_sift.c).
 //  * window positions are processed 64 at a time in raster order: each lane computes one
 //    position's gradient, weight, bins and its eight trilinear contributions (the per-pixel
 //    math, in parallel); the valid ones are compacted into LDS in raster order;
@@ -1479,85 +1266,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
 }
 
-// ------------------------------------------------------- brute-force kNN (k = 2)
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-
-VO_DEV bf16x8 load_frag(const float* row, int k0, int& sq)
-{
-    const float4 a = *reinterpret_cast<const float4*>(row + k0);
-    const float4 b = *reinterpret_cast<const float4*>(row + k0 + 4);
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    bf16x8 f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        f[j] = (__bf16)v[j];
-        const int iv = (int)v[j];
-        sq += iv * iv;
-    }
-    return f;
-}
-
-// one wave: 32 queries x all train rows in tiles of 32; block = 4 waves
-__global__ void __launch_bounds__(256) k_bf_knn2(const float* __restrict__ q, const int32_t* nq_p, const float* __restrict__ t,
-                                                 const int32_t* nt_p, int32_t* idx2, float* dist2)
-{
-    __shared__ float sd[4][32][33];
-    __shared__ int qn[4][32];
-    const int nq = *nq_p, nt = *nt_p;
-    const int w = wave_id(), lane = lane_id();
-    const int qbase = (blockIdx.x * 4 + w) * 32;
-    if (qbase >= nq) return;
-    const int r = lane & 31, h = lane >> 5;
-    const bool qv = qbase + r < nq;
-    const float* qrow = q + (int64_t)(qv ? qbase + r : qbase) * 128;
-    bf16x8 afr[8];
-    int sqa = 0;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) afr[s] = load_frag(qrow, 16 * s + 8 * h, sqa);
-    sqa += __shfl_xor(sqa, 32, 64);
-    if (h == 0) qn[w][r] = qv ? sqa : 0;
-    float d0 = FLT_MAX, d1 = FLT_MAX;
-    int i0 = -1, i1 = -1;
-    for (int t0 = 0; t0 < nt; t0 += 32) {
-        const int tr = t0 + r;
-        const float* trow = t + (int64_t)(tr < nt ? tr : t0) * 128;
-        f32x16 acc = {};
-        int sqb = 0;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const bf16x8 bfr = load_frag(trow, 16 * s + 8 * h, sqb);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[s], bfr, acc, 0, 0, 0);
-        }
-        sqb += __shfl_xor(sqb, 32, 64);
-        // C layout: col = lane & 31 (train), row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5) (query)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const int d2 = qn[w][row] + sqb - 2 * (int)acc[reg];
-            sd[w][row][r] = sqrtf((float)d2);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        if (h == 0) {
-            const int lim = min(32, nt - t0);
-            for (int c = 0; c < lim; ++c) {
-                const float d = sd[w][r][c];
-                if (d < d1) {
-                    if (d0 > d) { d1 = d0; i1 = i0; d0 = d; i0 = t0 + c; }
-                    else { d1 = d; i1 = t0 + c; }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (h == 0 && qv) {
-        const int qi = qbase + r;
-        idx2[2 * qi] = i0; idx2[2 * qi + 1] = i1;
-        dist2[2 * qi] = d0; dist2[2 * qi + 1] = d1;
-    }
-}
-
 // ratio test + gathering (:218-245), ordered by query index
 __global__ void __launch_bounds__(256) k_ratio(const float* kp0, const float* kp1, int kps, const int32_t* idx2,
                                               const float* dist2, const int32_t* nq_p, int qs, double ratio,
@@ -1726,35 +1434,16 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
     for (int o = 0; o < sb->n_oct; ++o) {
         const int w = sb->oct_w[o], h = sb->oct_h[o];
         if (w <= 2 * SIFT_IMG_BORDER || h <= 2 * SIFT_IMG_BORDER) continue;
-        // tiled, all layers of the octave per launch (VO_SIFT_EXTREMA_ROW=1: a thread per pixel
-        // and layer, the first form; same candidate set)
-        static const int ex_row = [] { const char* e = getenv("VO_SIFT_EXTREMA_ROW"); return e ? atoi(e) : 0; }();
-        if (ex_row == 1) {
-            for (int i = 1; i <= N_LAYERS; ++i)
-                hipLaunchKernelGGL(k_extrema, dim3((w - 2 * SIFT_IMG_BORDER + 127) / 128, h - 2 * SIFT_IMG_BORDER, nb),
-                                   dim3(128), 0, st, *sb, o, i);
-        } else {
-            const dim3 g((w - 2 * SIFT_IMG_BORDER + EX_W - 1) / EX_W, (h - 2 * SIFT_IMG_BORDER + EX_H - 1) / EX_H, nb);
-            hipLaunchKernelGGL(k_extrema_t, g, dim3(256), 0, st, *sb, o);
-        }
+        // tiled, all layers of the octave per launch
+        const dim3 g((w - 2 * SIFT_IMG_BORDER + EX_W - 1) / EX_W, (h - 2 * SIFT_IMG_BORDER + EX_H - 1) / EX_H, nb);
+        hipLaunchKernelGGL(k_extrema_t, g, dim3(256), 0, st, *sb, o);
     }
-    const char* kser = getenv("VO_SIFT_KP_SERIAL");
-    if (kser && atoi(kser) == 1) {
-        hipLaunchKernelGGL(k_sift_kp, dim3((sb->cand_cap + 127) / 128, 1, nb), dim3(128), 0, st, *sb);
-    } else {
-        hipLaunchKernelGGL(k_sift_refine, dim3((sb->cand_cap + 127) / 128, 1, nb), dim3(128), 0, st, *sb);
-        hipLaunchKernelGGL(k_sift_ori, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
-    }
+    hipLaunchKernelGGL(k_sift_refine, dim3((sb->cand_cap + 127) / 128, 1, nb), dim3(128), 0, st, *sb);
+    hipLaunchKernelGGL(k_sift_ori, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
     hipLaunchKernelGGL(k_sift_sort_dedupe, dim3(1, 1, nb), dim3(1024), 0, st, *sb);
     if (sb->nfeatures > 0)
         hipLaunchKernelGGL(k_sift_retain_best, dim3(1, 1, nb), dim3(RB_T), 0, st, *sb);
-    // wave-per-keypoint descriptor kernel unless VO_SIFT_DESC_SERIAL=1 (thread per keypoint;
-    // both produce identical descriptors)
-    const char* ser = getenv("VO_SIFT_DESC_SERIAL");
-    if (ser && atoi(ser) == 1)
-        hipLaunchKernelGGL(k_sift_desc, dim3((sb->kp_cap + 63) / 64, 1, nb), dim3(64), 0, st, *sb);
-    else
-        hipLaunchKernelGGL(k_sift_desc_w, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
+    hipLaunchKernelGGL(k_sift_desc_w, dim3(SIFT_WAVE_BLOCKS, 1, nb), dim3(256), 0, st, *sb);
     return hip_rc();
 }
 
@@ -1783,15 +1472,6 @@ extern "C" int vo_sift_retain_best_rows(float* kp_out, int32_t n, int32_t nfeatu
 extern "C" int vo_sift(const vo_sift_buf* sb, const uint8_t* img, int W, int H, vo_stream_t stream)
 {
     return vo_sift_batch(sb, 1, img, (int64_t)W * H, W, H, stream);
-}
-
-extern "C" int vo_bf_knn2(const float* q, const int32_t* nq, const float* t, const int32_t* nt, int32_t qcap,
-                          int32_t dim, int32_t* idx2, float* dist2, vo_stream_t stream)
-{
-    if (!q || !nq || !t || !nt || !idx2 || !dist2 || dim != 128 || qcap < 0) return VO_EARG;
-    if (qcap == 0) return VO_OK;
-    hipLaunchKernelGGL(k_bf_knn2, dim3((qcap + 127) / 128), dim3(256), 0, VO_STREAM(stream), q, nq, t, nt, idx2, dist2);
-    return hip_rc();
 }
 
 extern "C" int vo_ratio_matches(int B, const float* kp0, const float* kp1, int32_t kp_stride, const int32_t* idx2,

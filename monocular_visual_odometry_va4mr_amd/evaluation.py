@@ -107,3 +107,68 @@ def shard_report(shards, centres, gt_positions, stitched=None, reference=None) -
             out["stitched"]["ate_rmse"] = segs[0]["ate_rmse"]
             out["stitched"]["ate_rel"] = segs[0]["ate_rel"]
     return out
+
+
+def load_shard_cut(path: str, n_shards: int) -> dict | None:
+    """One cut of a shard fixture (tests/golden/kitti_seq00_shards*.npz, written by
+    make_long_golden.py from the reference class's own runs): per shard its (start, boot1,
+    end) bounds and, per pose from the bootstrap pose on, t_CW and (num_pts, landmarks,
+    candidates), plus the reference's error string ("" when it ran to the shard's end)."""
+    import os
+    if not os.path.exists(path):
+        return None
+    g = np.load(path, allow_pickle=False)
+    key = f"s{n_shards}"
+    if f"{key}_t" not in g.files:
+        return None
+    return {"bounds": g[f"{key}_bounds"], "t": g[f"{key}_t"], "counts": g[f"{key}_counts"],
+            "off": g[f"{key}_off"], "error": g[f"{key}_error"]}
+
+
+def chains_vs_shard_cut(cut: dict, starts, gap: int, pose_t, num_pts, nF, nL, nC, status, max_diffs: int = 16) -> dict:
+    """Compare batched chains with the reference runs of a shard cut.
+
+    A chain whose bootstrap frames [s, s + gap] are those of a shard of the cut ran exactly that
+    shard's frames (the bench's chain g takes frame s_g + gap + j - 1 at step j >= 2, as the
+    shard does), so its poses must equal the reference's pose for pose.  Per such chain, over
+    the poses both have: every t_CW (pose 0 is the identity at s), num_pts; when the reference
+    covers every pose of the chain, also the final landmark / candidate counts; a chain that
+    still tracks where the reference crashed counts as different.  Arrays are the engine's:
+    pose_t [B, fcap, 3] f64, num_pts [B, fcap] i32, nF / nL / nC / status [B]."""
+    pose_t, num_pts = np.asarray(pose_t), np.asarray(num_pts)
+    nF, nL, nC, status = (np.asarray(a).reshape(-1) for a in (nF, nL, nC, status))
+    by_start = {int(b[0]): k for k, b in enumerate(cut["bounds"]) if int(b[1]) - int(b[0]) == gap}
+    off = cut["off"]
+    compared = identical = full = 0
+    diffs = []
+    for g, s in enumerate(starts):
+        k = by_start.get(int(s))
+        if k is None:
+            continue
+        t = cut["t"][off[k]:off[k + 1]]                 # poses 1 .. of the shard
+        cnt = cut["counts"][off[k]:off[k + 1]]
+        err = str(cut["error"][k])
+        n = int(nF[g])                                  # chain poses incl. the identity
+        m = min(n - 1, len(t))
+        compared += 1
+        ok = n >= 2 and bool(np.all(pose_t[g, 0] == 0.0))
+        first = None
+        if ok:
+            eq = np.all(pose_t[g, 1:1 + m] == t[:m], axis=1) & (num_pts[g, 1:1 + m] == cnt[:m, 0])
+            if not eq.all():
+                ok, first = False, int(np.argmin(eq)) + 1
+        covered = m == n - 1
+        if ok and covered:
+            full += 1
+            if err and len(t) == m:
+                # the reference crashed at its next frame: the chain must have stopped there too
+                ok = int(status[g]) != 0 or n - 1 == 0
+            else:
+                ok = int(nL[g]) == int(cnt[m - 1, 1]) and int(nC[g]) == int(cnt[m - 1, 2]) and int(status[g]) == 0
+            first = None if ok else n - 1
+        elif ok and err:                               # the reference crashed before this chain's end
+            ok, first = False, m + 1
+        identical += int(ok)
+        if not ok and len(diffs) < max_diffs:
+            diffs.append({"chain": int(g), "shard": int(k), "first_pose": first, "status": int(status[g])})
+    return {"compared": compared, "identical": identical, "covering_every_pose": full, "differences": diffs}

@@ -120,10 +120,21 @@ def _scratch(dev, nbytes: int) -> torch.Tensor:
     return buf
 
 
-def bf_knn2_batch(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor):
+def matcher_scratch_bytes(B: int, qcap: int, tcap: int) -> int:
+    """Device bytes bf_knn2_batch needs for B problems of qcap x tcap descriptors."""
+    n = int(L.lib().vo_bf_knn2_batch_scratch(int(B), int(qcap), int(tcap)))
+    if n <= 0:
+        raise ValueError("bad matcher sizes")
+    return n
+
+
+def bf_knn2_batch(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor,
+                  scratch: torch.Tensor | None = None):
     """k=2 nearest neighbours for B problems on MFMA (vo_bf_knn2_batch).
     q [B,qcap,128] / t [B,tcap,128] float32 integer-valued descriptors, nq / nt int32 [B] device
-    counts; returns idx2 [B,qcap,2] i32 (-1 absent), dist2 [B,qcap,2] f32 (FLT_MAX absent)."""
+    counts; returns idx2 [B,qcap,2] i32 (-1 absent), dist2 [B,qcap,2] f32 (FLT_MAX absent).
+    ``scratch``: a uint8 device buffer the caller owns and uses only on this stream (an Engine
+    keeps one; ``matcher_scratch_bytes`` sizes it); None takes the per-stream cache."""
     if q.dim() != 3 or t.dim() != 3 or q.shape[2] != 128 or t.shape[2] != 128 or q.shape[0] != t.shape[0]:
         raise ValueError("q, t must be float32 [B, cap, 128] with the same B")
     dev = q.device
@@ -137,7 +148,12 @@ def bf_knn2_batch(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.
     nbytes = int(lib.vo_bf_knn2_batch_scratch(B, qcap, tcap))
     if nbytes <= 0:
         raise ValueError("bad matcher sizes")
-    scr = _scratch(dev, nbytes)
+    if scratch is not None:
+        if scratch.dtype != torch.uint8 or scratch.device != dev or scratch.numel() < nbytes:
+            raise ValueError(f"matcher scratch must be uint8 on {dev} with >= {nbytes} bytes")
+        scr = scratch
+    else:
+        scr = _scratch(dev, nbytes)
     st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     L.check(lib.vo_bf_knn2_batch(B, C.c_void_p(q.data_ptr()), C.c_void_p(nq.data_ptr()), qcap,
                                  C.c_void_p(t.data_ptr()), C.c_void_p(nt.data_ptr()), tcap, 128,
@@ -152,16 +168,3 @@ def bf_knn2(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor
     q = q[:qcap]
     i2, d2 = bf_knn2_batch(q[None], nq.reshape(1), t[None], nt.reshape(1))
     return i2[0], d2[0]
-
-
-def bf_knn2_reference(q: torch.Tensor, nq: torch.Tensor, t: torch.Tensor, nt: torch.Tensor, qcap: int):
-    """The single-problem kernel (vo_bf_knn2: one wave per 32 queries, train rows read from
-    global memory); kept as the second device implementation the batched one is tested against."""
-    dev = q.device
-    idx2 = torch.full((qcap, 2), -1, dtype=torch.int32, device=dev)
-    dist2 = torch.full((qcap, 2), float(np.finfo(np.float32).max), dtype=torch.float32, device=dev)
-    st = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    L.check(L.lib().vo_bf_knn2(C.c_void_p(q.data_ptr()), C.c_void_p(nq.data_ptr()), C.c_void_p(t.data_ptr()),
-                               C.c_void_p(nt.data_ptr()), qcap, 128, C.c_void_p(idx2.data_ptr()),
-                               C.c_void_p(dist2.data_ptr()), st), "vo_bf_knn2")
-    return idx2, dist2

@@ -124,6 +124,13 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
             return cache[torch.as_tensor([i - lo for i in ids], device=dev)]
         return renderer.render_batch(ids, Rs[ids], cs[ids])
 
+    boot0 = frames_at([s.start for s in mine])
+    boot1 = frames_at([s.boot1 for s in mine])
+    # the per-step layout and the two bootstrap frame sets hold every frame the run reads: the
+    # rank's frame cache is not needed any more (it doubled the frames' HBM)
+    if idx_dev is not None:
+        cache = None
+
     def step_frames(j, g):
         if idx_dev is not None:
             return steps[j, bounds[g]:bounds[g + 1]]
@@ -132,8 +139,6 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     def on(g):
         return torch.cuda.stream(streams[g]) if streams[g] is not None else _nullctx()
 
-    boot0 = frames_at([s.start for s in mine])
-    boot1 = frames_at([s.boot1 for s in mine])
     last = np.array([s.n_steps - 1 for s in mine])
     last_dev = [torch.as_tensor(last[bounds[g]:bounds[g + 1]], device=dev) for g in range(G)]
     # the SIFT workspace is allocated before the clock, as the reference creates its SIFT in

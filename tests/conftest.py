@@ -42,3 +42,17 @@ def golden_frames(g):
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+@pytest.fixture
+def launch_cus():
+    """Set the CU count the C ABI's launch-shape decisions assume (vo_set_launch_cus); 1 puts a
+    small batch on the many-chains forms (one block per chain: k_essential<2>, k_recover_pose,
+    the one-block k_triangulate, k_pnp_tri<2 waves/EU>).  Restored to the device's own count."""
+    from monocular_visual_odometry_va4mr_amd import _lib as L
+
+    def set_(n):
+        L.check(L.lib().vo_set_launch_cus(int(n)), "vo_set_launch_cus")
+
+    yield set_
+    set_(0)

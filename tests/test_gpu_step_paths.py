@@ -1,7 +1,9 @@
-"""The step's three launch forms give the same state: the engine default (vo_track_lk +
+"""The step's launch forms give the same state: the engine default (vo_track_lk +
 vo_filter_pnp_triangulate), tracking with its own filtering launch (vo_track +
-vo_pnp_triangulate, VO_COMPACT_IN_TRACK=1) and the separate PnP / triangulation calls
-(vo_track + vo_pnp + vo_triangulate, fuse_pnp_tri = False) -- every C-ABI path of the step."""
+vo_pnp_triangulate, VO_COMPACT_IN_TRACK=1), the separate PnP / triangulation calls
+(vo_track + vo_pnp + vo_triangulate, fuse_pnp_tri = False) and the latency stages on a
+stream of their own (VO_PRIO_LATENCY=1), eager and replayed from a hipGraph -- every C-ABI
+path of the step, at both sides of the launch-shape threshold (vo_set_launch_cus)."""
 import numpy as np
 import pytest
 import torch
@@ -18,29 +20,47 @@ def _run(frames, starts, K, opts, n_steps, form, monkeypatch):
         monkeypatch.setenv("VO_COMPACT_IN_TRACK", "1")
     else:
         monkeypatch.delenv("VO_COMPACT_IN_TRACK", raising=False)
+    if form.startswith("prio_latency"):            # PnP + finish on a high-priority stream of their own
+        monkeypatch.setenv("VO_PRIO_LATENCY", "1")
+    else:
+        monkeypatch.delenv("VO_PRIO_LATENCY", raising=False)
     eng = Engine(K, opts, 1241, 376, batch=len(starts), ncap=4096, pcap=8192, fcap=16)
     if form == "split":
         eng.fuse_pnp_tri = False
     eng.bootstrap(frames[starts], frames[[s + 2 for s in starts]])
     snaps = []
+    graph = form.endswith("graph")
+    if graph:
+        eng.capture_step()
     for j in range(n_steps):
-        eng.step(frames[[s + 3 + j for s in starts]])
+        f = frames[[s + 3 + j for s in starts]]
+        if graph:
+            eng.step_graph(f)
+        else:
+            eng.step(f)
         torch.cuda.synchronize()
         snaps.append({k: eng.t[k].cpu().numpy().copy() for k in KEYS})
     return snaps
 
 
-def test_step_launch_forms_agree(monkeypatch):
+@pytest.mark.parametrize("cus", [0, 1])
+def test_step_launch_forms_agree(monkeypatch, launch_cus, cus):
+    """cus = 1: every launch takes the many-chains form (k_pnp_tri / k_pnp_fused at 2 waves
+    per EU, the one-block triangulation) -- the forms of the 768-chain headline; the default
+    run (cus = 0, the device's own count) takes the unconstrained builds.  Both are compared
+    with the same reference run (default form, default threshold)."""
     from monocular_visual_odometry_va4mr_amd import options as Op
     from monocular_visual_odometry_va4mr_amd.synth import make_sequence
     fr, K, _, _ = make_sequence("kitti", 14, seed=1)
     opts, _, _ = Op.get("kitti")
     frames = torch.from_numpy(np.ascontiguousarray(fr)).cuda()
     starts = [0, 1, 3]
-    runs = {f: _run(frames, starts, K, opts, 7, f, monkeypatch) for f in ("default", "compact_in_track", "split")}
-    ref = runs["default"]
+    ref = _run(frames, starts, K, opts, 7, "default", monkeypatch)
     assert (ref[-1]["status"] == 0).all()
-    for f in ("compact_in_track", "split"):
+    launch_cus(cus)
+    forms = ("default", "compact_in_track", "split", "prio_latency", "graph", "prio_latency_graph")
+    runs = {f: _run(frames, starts, K, opts, 7, f, monkeypatch) for f in forms}
+    for f in forms:
         for j, (a, b) in enumerate(zip(ref, runs[f])):
             for k in KEYS:
                 assert np.array_equal(a[k], b[k]), f"{f}: step {j} {k}"

@@ -6,8 +6,7 @@
 B problems of n x n SIFT-like descriptors (non-negative, L2 norm ~512, clipped to 255 and
 rounded, as cv::SIFT writes them) per launch of vo_bf_knn2_batch.  Reports pairs/s and the
 MFMA rate of the whole call (prep + MFMA + merge) and of the k_bf_mfma kernel alone
-(2 * n * n * 128 FLOP per problem) against the bf16 dense peak; the single-problem kernel
-(vo_bf_knn2) is timed beside it.  Prints one JSON line."""
+(2 * n * n * 128 FLOP per problem) against the bf16 dense peak.  Prints one JSON line."""
 import argparse
 import json
 import os
@@ -18,7 +17,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch, bf_knn2_reference  # noqa: E402
+from monocular_visual_odometry_va4mr_amd.features import bf_knn2_batch  # noqa: E402
 
 PEAK_BF16 = 2.5e15      # dense bf16 MFMA, MI355X (MI355X_MICROARCH.md)
 
@@ -36,7 +35,6 @@ def main():
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--ref", type=int, default=1, help="also time the single-problem kernel")
     a = ap.parse_args()
     dev = torch.device("cuda")
     rng = np.random.default_rng(7)
@@ -58,21 +56,6 @@ def main():
     out = {"tool": "match_bench", "B": a.B, "n": a.n, "ms_per_call": round(ms, 4),
            "pairs_per_s": round(a.B / (ms * 1e-3), 1), "tflops_call": round(flop / (ms * 1e-3) / 1e12, 2),
            "mfma_frac_call": round(flop / (ms * 1e-3) / PEAK_BF16, 4)}
-    if a.ref:
-        q0, t0 = q[0].contiguous(), t[0].contiguous()
-        bf_knn2_reference(q0, nq[:1], t0, nt[:1], a.n)
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(3):
-            bf_knn2_reference(q0, nq[:1], t0, nt[:1], a.n)
-        e1.record()
-        torch.cuda.synchronize()
-        rms = e0.elapsed_time(e1) / 3
-        out["single_kernel_ms_per_pair"] = round(rms, 4)
-        out["single_kernel_tflops"] = round(2.0 * a.n * a.n * 128 / (rms * 1e-3) / 1e12, 2)
-        i2, _ = bf_knn2_batch(q[:1], nq[:1], t[:1], nt[:1])
-        ri, _ = bf_knn2_reference(q0, nq[:1], t0, nt[:1], a.n)
-        out["batch_equals_single"] = bool(torch.equal(i2[0], ri))
     print(json.dumps(out), flush=True)
 
 

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """SIFT detectAndCompute time per image (vo_sift) on KITTI / Malaga-1024 / 1080p synthetic
-frames, thread-per-keypoint vs wave-per-keypoint descriptor kernel (VO_SIFT_DESC_SERIAL),
-plus one SIFT+SIFT+BF-match pair (BASELINE config C3).  Prints one JSON line per size."""
+frames, plus one SIFT+SIFT+BF-match pair (BASELINE config C3).  Prints one JSON line per size."""
 import json
 import os
 import sys
@@ -37,9 +36,7 @@ def main():
         s0 = Sift(a.shape[1], a.shape[0], "cuda")
         s1 = Sift(a.shape[1], a.shape[0], "cuda")
         res = {"preset": preset, "W": a.shape[1], "H": a.shape[0]}
-        for mode in ("1", "0"):
-            os.environ["VO_SIFT_DESC_SERIAL"] = mode
-            res["ms_per_image_" + ("serial_desc" if mode == "1" else "wave_desc")] = round(timed(lambda: s0.run(a), iters), 3)
+        res["ms_per_image"] = round(timed(lambda: s0.run(a), iters), 3)
         s0.run(a)
         s1.run(b)
         torch.cuda.synchronize()
