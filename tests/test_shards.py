@@ -270,3 +270,28 @@ def test_run_sequence_world_x_bseq_plan_gloo_world2():
     assert st["coverage_breaks"] == [[0, 2, 1]]
     assert [s["shards"] for s in st["segments"]] == [[0], [2, 3, 4, 5, 6, 7]]
     assert all(s["ate_rel"] < 1e-9 for s in st["segments"])
+
+
+@pytest.mark.parametrize("n_shards,drop", [(3, []), (8, [3]), (64, [1, 2]), (256, [100]), (256, [])])
+def test_batched_stitch_equals_shard_by_shard(n_shards, drop):
+    """stitch (batched Umeyama over all consecutive pairs + segmented prefix product) against
+    the shard-by-shard chaining it replaces (stitch_reference): same segments, breaks and
+    coverage, positions equal up to rounding -- with dropped shards (coverage breaks) and a
+    truncated first shard."""
+    n = 4541
+    gt = _traj(n, seed=3)
+    rng = np.random.default_rng(n_shards)
+    sh = Sh.plan_shards(n, n_shards, gap=2, overlap=30)
+    cs = []
+    for k, s in enumerate(sh):
+        fr = np.array([s.start] + list(range(s.boot1, s.end)))
+        cs.append(_sim3(gt[fr], 0.5 + 0.01 * k, 0.1 * k, np.array([k, -k, 2.0 * k])) + rng.normal(0, 1e-3, (len(fr), 3)))
+    keep = [s for i, s in enumerate(sh) if i not in drop]
+    kc = [c for i, c in enumerate(cs) if i not in drop]
+    kc[0] = kc[0][:-5]
+    a, b = Sh.stitch_reference(keep, kc), Sh.stitch(keep, kc)
+    assert a.breaks == b.breaks and a.segments == b.segments
+    assert np.array_equal(a.segment, b.segment)
+    m = ~np.isnan(a.positions[:, 0])
+    assert np.array_equal(m, ~np.isnan(b.positions[:, 0]))
+    assert np.allclose(a.positions[m], b.positions[m], rtol=0, atol=1e-9 * (1 + np.abs(a.positions[m]).max()))
