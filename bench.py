@@ -83,6 +83,8 @@ def parse():
                     help="shards per GPU of the whole-sequence job (n_shards = world x this; default "
                          "seq_chains_for(world))")
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
+    ap.add_argument("--no-rank-slices", action="store_true",
+                    help="skip the one-rank-of-N sequence slices (rank 0 of world 2 / 4 / 8 on this GPU)")
     # 8 hardware queues per process (HIP's default is 4): the legs' stream groups then no longer
     # share queues by accident of the process's stream history -- the sequence leg kept 29.6-29.7k
     # frames/s after a captured one-chain step instead of dropping to 25.8k; every leg measured
@@ -344,6 +346,59 @@ def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3):
             "reference_fixture": vs is not None,
             "stitched_frames": st.get("frames"), "coverage_breaks": st.get("coverage_breaks"),
             "stitched_ate_rel_vs_gt": st.get("ate_rel")}
+
+
+def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3):
+    """What one rank of an N-GPU sequence job does, measured on this GPU:
+    rank 0's slice of the world = N plan (N x seq_chains_for(N) shards of the C2 sequence; for
+    N = 8, shards 0..31 of the 256-shard cut) run alone, bootstrap included, every shard
+    compared with the reference class's run on the same boundaries.  Ranks hold equal slices
+    and run independently until the final gather, so the job's predicted rate is SEQ_LEN / the
+    rank's wall; `..._incl_stitch` adds the batched stitch of all N x B shards (timed on the
+    reference cut's own poses) -- the RCCL gather of ~0.4 MB is not modelled.  Median of `reps`
+    runs per N, every run's wall listed."""
+    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
+    out = {}
+    for world in worlds:
+        per_gpu = seq_chains_for(world)
+        n_shards = world * per_gpu
+        ref = None
+        for name in ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz"):
+            ref = ref or reference_shards(os.path.join(ROOT, "tests", "golden", name), n_shards)
+        runs = []
+        for _ in range(reps):
+            r = run("kitti", SEQ_LEN, per_gpu, overlap=30, seed=seed, device=device, rank=0, world=world,
+                    reference=ref, time_boot=False)
+            runs.append(r)
+            torch.cuda.empty_cache()
+        res = sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2]
+        stitch_ms = stitch_time_ms(ref, n_shards) if ref else None
+        vs = res.get("vs_reference") or {}
+        out[str(world)] = {
+            "shards_total": n_shards, "rank0_shards": res["shards"], "groups": res["groups"],
+            "per_rank_wall_s": res["wall_s"], "wall_s_runs": [r["wall_s"] for r in runs],
+            "bootstrap_s": res["bootstrap_s"], "steps": res["steps"],
+            "ms_per_step": round(res["step_s"] / max(1, res["steps"]) * 1e3, 4),
+            "predicted_frames_per_s": round(SEQ_LEN / res["wall_s"], 1),
+            "stitch_ms_all_shards": stitch_ms,
+            "predicted_frames_per_s_incl_stitch": (round(SEQ_LEN / (res["wall_s"] + stitch_ms * 1e-3), 1)
+                                                   if stitch_ms is not None else None),
+            "shards_ok": res["shards_ok"], "shards_compared": vs.get("shards_compared"),
+            "shards_identical": vs.get("shards_identical")}
+    return out
+
+
+def stitch_time_ms(ref: dict, n_shards: int, iters: int = 5) -> float:
+    """Median wall of shards.stitch over the reference cut's own per-shard positions (the
+    input rank 0 stitches after the gather, at the job's full shard count)."""
+    plan = Sh.plan_shards(SEQ_LEN, n_shards, 2, 30)
+    cs = [ref[k] for k in range(n_shards)]
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        Sh.stitch(plan, cs)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return round(float(np.median(ts)), 3)
 
 
 def cpu_baseline(K, opts, frames_np, gap):
@@ -614,6 +669,11 @@ def main():
                                groups=args.seq_groups)
         except Exception as exc:  # noqa: BLE001
             seq = {"error": f"{type(exc).__name__}: {exc}"}
+        if world == 1 and not args.no_rank_slices and "error" not in (seq or {}):
+            try:
+                seq["rank_slices"] = rank_slice_leg(device, args.seed)
+            except Exception as exc:  # noqa: BLE001
+                seq["rank_slices"] = {"error": f"{type(exc).__name__}: {exc}"}
 
     if rank != 0:
         if dist is not None:

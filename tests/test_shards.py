@@ -295,3 +295,20 @@ def test_batched_stitch_equals_shard_by_shard(n_shards, drop):
     m = ~np.isnan(a.positions[:, 0])
     assert np.array_equal(m, ~np.isnan(b.positions[:, 0]))
     assert np.allclose(a.positions[m], b.positions[m], rtol=0, atol=1e-9 * (1 + np.abs(a.positions[m]).max()))
+
+
+def test_run_sequence_rank_slice_without_process_group():
+    """world > 1 without torch.distributed: the process runs rank r's slice of the world-size
+    plan alone (bench.py's rank_slices: one GPU standing in for one rank of an N-GPU job); the
+    report covers exactly that slice's shards."""
+    from monocular_visual_odometry_va4mr_amd.run_sequence import run
+    plan = Sh.plan_shards(200, 3 * 2, 2, 30)
+    _StubEngine.fail_start = -1
+    for rank in range(3):
+        rep = run("parking", 200, 2, overlap=30, device="cpu", rank=rank, world=3, engine_cls=_StubEngine,
+                  renderer=_StubRenderer(), prerender=False)
+        mine = Sh.rank_shards(plan, rank, 3)
+        assert rep["slice_of_rank"] == rank and rep["shards"] == len(mine) == 2
+        assert [s.index for s in rep["_plan"]] == [s.index for s in mine]
+        assert rep["shards_ok"] == 2 and rep["failed_shards"] == []
+        assert rep["stitched"]["coverage_breaks"] == []
