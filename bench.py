@@ -85,12 +85,11 @@ def parse():
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
     ap.add_argument("--no-rank-slices", action="store_true",
                     help="skip the one-rank-of-N sequence slices (rank 0 of world 2 / 4 / 8 on this GPU)")
-    # 8 hardware queues per process (HIP's default is 4): the legs' stream groups then no longer
-    # share queues by accident of the process's stream history -- the sequence leg kept 29.6-29.7k
-    # frames/s after a captured one-chain step instead of dropping to 25.8k; every leg measured
-    # equal or slightly faster (profiles/r4_hw_queues.txt).  0 leaves the environment's value.
-    ap.add_argument("--hw-queues", type=int, default=8,
-                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; <= 32; 0 = leave)")
+    # hardware queues: the package sets GPU_MAX_HW_QUEUES=8 at import unless the environment
+    # has a value (monocular_visual_odometry_va4mr_amd/__init__.py); --hw-queues N overrides it
+    # for experiments (set before HIP initialises; <= 32)
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0 = the package's / environment's value)")
     return ap.parse_args()
 
 
