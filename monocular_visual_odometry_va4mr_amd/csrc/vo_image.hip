@@ -654,7 +654,7 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
 template <int WW, int WH>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd, int boff)
 {
     constexpr int WPB = 1;
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
@@ -695,7 +695,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     for (level = level_hi; level >= level_lo; --level)
         for (int k = 2; k < 8; ++k) LKPROF_SET(k, 0);
     level = level_lo;
-    if (!lk_block(B, nb, b, pb, xcd != 0, (int)blockIdx.x * WPB + wv)) return;
+    if (!lk_block(B, nb, b, pb, xcd != 0, (boff + (int)blockIdx.x) * WPB + wv)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
     const int n0 = P.n0 ? P.n0[b] : 0;
     int n1 = P.n1 ? P.n1[b] : 0;
@@ -2157,7 +2157,16 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     // sizes (cv2.calcOpticalFlowPyrLK's default 21x21 on the cv2compat surface): k_lk, one
     // launch per level.
     if (staged15) {
-        hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
+        // VO_LK_CHUNKS = n (measurement option): the grid as n launches over consecutive chain
+        // ranges; between them the stream drains, and other streams' blocks can take the freed
+        // wave slots and LDS (results identical)
+        static const int chunks_env = [] { const char* e = getenv("VO_LK_CHUNKS"); return e ? atoi(e) : 1; }();
+        const int nch = chunks_env > 1 && !xcd_env ? chunks_env : 1;
+        const int per = ((nblk / nb + nch - 1) / nch) * nb;          // whole chains per launch
+        for (int c0 = 0; c0 < nblk; c0 += per) {
+            const int n = nblk - c0 < per ? nblk - c0 : per;
+            hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(n), dim3(64), 0, st, P, L, 0, B, nb, xcd_env, c0);
+        }
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {
