@@ -17,6 +17,7 @@ KITTI-length synthetic C2 sequence (4541 frames, seed 1):
 Frames are rendered once into a raw memmap (every frame's SHA-1 is stored, so the GPU
 tests can check their own renders), then the reference runs are spread over processes.
 Usage:  python tests/golden/make_long_golden.py [--procs 8] [--cuts 8,16] [--no-full] [--out FILE]
+        [--overlap O]   (kitti_seq00_shards_o15.npz: the overlap study's 15-frame cuts)
 """
 from __future__ import annotations
 
@@ -99,6 +100,7 @@ def main():
     ap.add_argument("--cuts", default=",".join(str(c) for c in SHARD_COUNTS), help="shard counts")
     ap.add_argument("--no-full", action="store_true", help="skip the one-chain run (kitti_seq00.npz)")
     ap.add_argument("--out", default="kitti_seq00_shards.npz", help="shard fixture file (merged)")
+    ap.add_argument("--overlap", type=int, default=OVERLAP, help="frames shared by neighbouring shards")
     a = ap.parse_args()
     cuts = [int(c) for c in a.cuts.split(",") if c]
     from monocular_visual_odometry_va4mr_amd import options as O
@@ -121,7 +123,7 @@ def main():
     _, (b0, b1), _ = O.get(PRESET)
     gap = b1 - b0
     jobs = [] if a.no_full else [("full", 0, gap, N_FRAMES, shape)]
-    plans = {S: Sh.plan_shards(N_FRAMES, S, gap, OVERLAP) for S in cuts}
+    plans = {S: Sh.plan_shards(N_FRAMES, S, gap, a.overlap) for S in cuts}
     for S, plan in plans.items():
         jobs += [(f"s{S}_{s.index}", s.start, s.boot1, s.end, shape) for s in plan]
     # longest runs first so the pool's tail is short
@@ -137,9 +139,11 @@ def main():
                             boot=np.array([b0, b1]), t=full_t, num_pts=full_cnt[:, 0], N=full_cnt[:, 1],
                             P=full_cnt[:, 2], error=np.asarray(full_err), digests=digests)
     out_path = os.path.join(HERE, a.out)
-    out = {"preset": PRESET, "seed": SEED, "n_frames": N_FRAMES, "overlap": OVERLAP}
+    out = {"preset": PRESET, "seed": SEED, "n_frames": N_FRAMES, "overlap": a.overlap}
     if os.path.exists(out_path):
         old = np.load(out_path, allow_pickle=False)
+        if int(old["overlap"]) != a.overlap:
+            raise SystemExit(f"{out_path} holds overlap {int(old['overlap'])}, not {a.overlap}")
         out.update({k: old[k] for k in old.files if k.startswith("s") and k.split("_")[0][1:].isdigit()})
     for S, plan in plans.items():
         ts, offs, errs, cnts = [], [0], [], []

@@ -183,6 +183,64 @@ def test_lk_bitexact(kitti_frames, engine_factory):
     assert np.array_equal(err.cpu().numpy()[0][m], re[m])
 
 
+def test_lk_bitexact_many_chains_under_load():
+    """LK at the headline's occupancy: 96 chains, each a different frame
+    pair of the C2 sequence with its GFTT corners, random and sub-pixel-jittered points, tracked
+    in one k_lk_w launch (96 x 2048 one-wave blocks, 8 waves per SIMD) while a second stream
+    tracks another 96-chain batch concurrently; every point of every chain of both batches
+    against the CPU restatement.  A single pair at one chain cannot see an LDS-ordering or
+    counter hazard that only shows when LDS latency is long."""
+    import ctypes as C
+    from oracle import _olib as O
+    from monocular_visual_odometry_va4mr_amd import options as Op
+    from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    fr, K, _, _ = make_sequence("kitti", 13, seed=1)
+    opts, _, _ = Op.get("kitti")
+    B, cap = 96, 2048
+    rng = np.random.default_rng(11)
+    runs = []
+    for r in range(2):
+        eng = Engine(K, opts, 1241, 376, batch=B, ncap=cap, pcap=cap, fcap=8)
+        pairs = [((b + 5 * r) % 12, (b + 5 * r) % 12 + 1) for b in range(B)]
+        pts = np.zeros((B, cap, 2), np.float32)
+        cnt = np.zeros(B, np.int32)
+        for b, (i, _) in enumerate(pairs):
+            g = O.gftt(fr[i], 1400, 0.05, 7)[: cap - 500]
+            extra = np.c_[rng.uniform(-30, 1270, 250), rng.uniform(-30, 400, 250)].astype(np.float32)
+            tiny = (g[:250] + np.float32([[1e-3, 2e-3]]) * rng.integers(1, 8, (min(250, len(g)), 2))).astype(np.float32)
+            p = np.concatenate([g, extra, tiny])
+            pts[b, :len(p)] = p
+            cnt[b] = len(p)
+        eng.build_pyramid(torch.from_numpy(np.stack([fr[i] for i, _ in pairs])), 0)
+        eng.build_pyramid(torch.from_numpy(np.stack([fr[j] for _, j in pairs])), 1)
+        d = {"pts": torch.from_numpy(pts).cuda(), "cnt": torch.from_numpy(cnt).cuda(),
+             "out": torch.zeros(B, cap, 2, device="cuda"), "st": torch.zeros(B, cap, dtype=torch.uint8, device="cuda"),
+             "err": torch.zeros(B, cap, device="cuda")}
+        runs.append((eng, pairs, pts, cnt, d))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for (eng, _, _, _, d), s in zip(runs, streams):
+        with torch.cuda.stream(s):
+            rc = eng.lib.vo_lk_points(eng._pd, eng._po, eng._ps, 0, C.c_void_p(d["pts"].data_ptr()),
+                                      C.c_void_p(d["cnt"].data_ptr()), cap, C.c_void_p(d["out"].data_ptr()),
+                                      C.c_void_p(d["st"].data_ptr()), C.c_void_p(d["err"].data_ptr()), eng.stream)
+            assert rc == 0
+    torch.cuda.synchronize()
+    bad = []
+    for eng, pairs, pts, cnt, d in runs:
+        out, st, err = d["out"].cpu().numpy(), d["st"].cpu().numpy(), d["err"].cpu().numpy()
+        for b, (i, j) in enumerate(pairs):
+            n = int(cnt[b])
+            ro, rs, re = O.lk(fr[i], fr[j], pts[b, :n], tuple(opts["winSize"]), opts["maxLevel"], opts["criteria"])
+            m = rs == 1
+            ok = (np.array_equal(st[b, :n], rs) and np.array_equal(out[b, :n], ro) and np.array_equal(err[b, :n][m], re[m]))
+            if not ok:
+                k = int(np.argmax(~np.all(out[b, :n] == ro, axis=1) | (st[b, :n] != rs)))
+                bad.append((b, i, j, k, pts[b, k].tolist()))
+    assert not bad, bad[:8]
+
+
 def test_pnp_ransac_matches_oracle(engine_factory):
     from oracle import _olib as O
     from monocular_visual_odometry_va4mr_amd import cv2compat as G
