@@ -395,8 +395,9 @@ class Engine:
         return self._sift, m
 
     def release_bootstrap(self):
-        """Free the SIFT workspace (stepping never needs it)."""
+        """Free the SIFT workspace and the matcher scratch (stepping never needs them)."""
         self._sift = None
+        self._mscr = None
         torch.cuda.empty_cache()
 
     def bootstrap(self, img0, img1, sift_batch_bytes: int | None = None):
@@ -411,7 +412,7 @@ class Engine:
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync: a chain
         whose SIFT keypoints hit the capacity ends with status VO_ST_CAPACITY."""
-        from .features import bf_knn2_batch
+        from .features import bf_knn2_batch, matcher_scratch_bytes
         img0 = self._frames(img0)
         img1 = self._frames(img1)
         d = self.dims
@@ -430,6 +431,11 @@ class Engine:
         n1 = torch.zeros_like(n0)
         ovf = torch.zeros(B, dtype=torch.int32, device=dev)      # per chain: SIFT capacity hit
         st = self.stream
+        # the matcher's scratch belongs to this engine: engines bootstrapping on
+        # their own streams never share one, and no allocation happens inside the chunk loop
+        mbytes = matcher_scratch_bytes(min(m, B), kcap, kcap)
+        if getattr(self, "_mscr", None) is None or self._mscr.numel() < mbytes:
+            self._mscr = torch.empty(mbytes, dtype=torch.uint8, device=dev)
         for c0 in range(0, B, m):
             c1 = min(B, c0 + m)
             k = c1 - c0
@@ -438,7 +444,7 @@ class Engine:
             ovf[c0:c1] = torch.maximum(flag[:k], flag[k:])
             n0[c0:c1] = n[:k]
             n1[c0:c1] = n[k:]
-            idx2, dist2 = bf_knn2_batch(desc[:k], n[:k], desc[k:], n[k:])
+            idx2, dist2 = bf_knn2_batch(desc[:k], n[:k], desc[k:], n[k:], scratch=self._mscr)
             self._chk(self.lib.vo_ratio_matches(k, C.c_void_p(kp[:k].data_ptr()), C.c_void_p(kp[k:].data_ptr()), kcap,
                                                 C.c_void_p(idx2.data_ptr()), C.c_void_p(dist2.data_ptr()),
                                                 C.c_void_p(n[:k].data_ptr()), kcap, float(self.opts.feature_ratio),
@@ -458,6 +464,7 @@ class Engine:
             # the caching allocator only reuses the blocks once the queued kernels are done
             # with them; dropping the references is stream-ordered, so no synchronisation
             self._sift = None
+            self._mscr = None
 
     # ------------------------------------------------------------------ state I/O
     def import_chain(self, b: int, *, landmarks, keypoints, cand, cand_first, cand_tau, transforms,
