@@ -433,7 +433,7 @@ class Engine:
         st = self.stream
         # the matcher's scratch belongs to this engine: engines bootstrapping on
         # their own streams never share one, and no allocation happens inside the chunk loop
-        mbytes = matcher_scratch_bytes(min(m, B), kcap, kcap)
+        mbytes = max(matcher_scratch_bytes(min(B, c0 + m) - c0, kcap, kcap) for c0 in {0, (B - 1) // m * m})
         if getattr(self, "_mscr", None) is None or self._mscr.numel() < mbytes:
             self._mscr = torch.empty(mbytes, dtype=torch.uint8, device=dev)
         for c0 in range(0, B, m):
