@@ -57,7 +57,29 @@ struct BfArgs {
     float* dist2;          // [B][qcap][2]
     int32_t* flag_n;       // fixup list length
     int32_t* flag_list;    // [B * qcap] b * qcap + q
+    // device work plan (int8 path, B <= BF_PLAN_MAXB): the splits come from the device counts, not
+    // the capacities, and the kernel's blocks loop over the (problem, query block, split) items
+    int planned;
+    int32_t* plan;         // [B + 2]: item prefix per problem, then the common split count
 };
+
+#define BF_PLAN_MAXB 1024   // problems the device plan handles (larger batches: capacity plan)
+#define BF_TARGET 2048      // work items the plan aims at (8 per CU)
+
+// Per-problem split of the planned path: nqb query blocks, sp train splits of `per` rows (a
+// multiple of the tile rows), from the counts and the batch-wide split count sp_all.
+struct BfPlan {
+    int nqb, sp, per;
+};
+VO_DEV BfPlan bf_plan(int nq, int nt, int sp_all, int tt)
+{
+    BfPlan p;
+    p.nqb = nq > 0 ? (nq + BF_QB - 1) / BF_QB : 0;
+    const int tiles = (nt + tt - 1) / tt;
+    p.sp = max(1, min(sp_all, tiles));
+    p.per = (((nt + p.sp - 1) / p.sp + tt - 1) / tt) * tt;
+    return p;
+}
 
 // train rows per split of a problem with nt rows (a multiple of the tile rows)
 VO_DEV int bf_per(int nt, const BfArgs& A) { return (((nt + A.tsplit - 1) / A.tsplit) + A.tt - 1) / A.tt * A.tt; }
@@ -244,35 +266,40 @@ struct BfPrep {
 };
 __global__ void __launch_bounds__(256) k_bf_prep_i8(BfPrep Q, BfPrep T, int B, int qblocks, int32_t* flag_n)
 {
-    const bool isq = (int)blockIdx.x < qblocks;
-    const BfPrep& X = isq ? Q : T;
-    const float* __restrict__ src = X.src;
-    const int32_t* n = X.n;
-    const int cap = X.cap;
-    int8_t* __restrict__ dst = X.dst;
-    int32_t* __restrict__ nrm = X.nrm;
     if (blockIdx.x == 0 && threadIdx.x == 0) *flag_n = 0;
-    const int row = ((int)blockIdx.x - (isq ? 0 : qblocks)) * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
-    const int b = row / cap, r = row - b * cap;
-    const bool ok = b < B && r < n[min(b, B - 1)];
-    int ss = 0;
-    if (ok) {
-        const float4* s4 = reinterpret_cast<const float4*>(src + (int64_t)row * 128 + 16 * part);
-        uint32_t w[4];
+    // grid-stride over the 32-row groups of both operands (queries first); a group past its
+    // problem's count is skipped with one load, so the grid need not cover the capacities
+    const int64_t gq = (int64_t)B * ((Q.cap + 31) / 32), gt = (int64_t)B * ((T.cap + 31) / 32);
+    (void)qblocks;
+    for (int64_t g = blockIdx.x; g < gq + gt; g += gridDim.x) {
+        const bool isq = g < gq;
+        const BfPrep& X = isq ? Q : T;
+        const int gpc = (X.cap + 31) / 32;
+        const int64_t gg = isq ? g : g - gq;
+        const int b = (int)(gg / gpc), r = (int)(gg - (int64_t)b * gpc) * 32 + (threadIdx.x >> 3), part = threadIdx.x & 7;
+        const int nb = X.n[b];
+        if ((int)(gg - (int64_t)b * gpc) * 32 >= nb) continue;           // block-uniform
+        const bool ok = r < nb && r < X.cap;
+        const int64_t row = (int64_t)b * X.cap + r;
+        int ss = 0;
+        if (ok) {
+            const float4* s4 = reinterpret_cast<const float4*>(X.src + row * 128 + 16 * part);
+            uint32_t w[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float4 v = s4[k];
-            const int a0 = (int)v.x - 128, a1 = (int)v.y - 128, a2 = (int)v.z - 128, a3 = (int)v.w - 128;
-            ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-            w[k] = (uint32_t)(a0 & 255) | ((uint32_t)(a1 & 255) << 8) | ((uint32_t)(a2 & 255) << 16) |
-                   ((uint32_t)(a3 & 255) << 24);
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = s4[k];
+                const int a0 = (int)v.x - 128, a1 = (int)v.y - 128, a2 = (int)v.z - 128, a3 = (int)v.w - 128;
+                ss += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+                w[k] = (uint32_t)(a0 & 255) | ((uint32_t)(a1 & 255) << 8) | ((uint32_t)(a2 & 255) << 16) |
+                       ((uint32_t)(a3 & 255) << 24);
+            }
+            *reinterpret_cast<uint4*>(X.dst + row * 128 + 16 * part) = make_uint4(w[0], w[1], w[2], w[3]);
         }
-        *reinterpret_cast<uint4*>(dst + (int64_t)row * 128 + 16 * part) = make_uint4(w[0], w[1], w[2], w[3]);
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        if (ok && part == 0) X.nrm[row] = ss;
     }
-    ss += __shfl_xor(ss, 1, 64);
-    ss += __shfl_xor(ss, 2, 64);
-    ss += __shfl_xor(ss, 4, 64);
-    if (ok && part == 0) nrm[row] = ss;
 }
 
 // middle of three (v_med3_i32): with hi >= lo, med3(hi, lo, v) = max(lo, min(hi, v))
@@ -299,19 +326,72 @@ __global__ void __launch_bounds__(256) k_bf_i8(BfArgs A)
     constexpr int NPRE = TT * 8 / 256;            // 16-byte slots per thread per tile
     __shared__ uint4 tile[2][TT * 8];             // TT rows x 128 B
     __shared__ int ntn[2][TT];                    // -|t'|^2 per row
-    const int nqb = (A.qcap + A.qb - 1) / A.qb;
-    int blk = blockIdx.x;
-    const int sp = blk % A.tsplit;
-    blk /= A.tsplit;
-    const int qb = blk % nqb, b = blk / nqb;
-    if (b >= A.B) return;
+    __shared__ int pref_s[BF_PLAN_MAXB + 1];      // planned path: work items before problem b
+    __shared__ int scan_s[16];
+    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
+    // Work items.  Planned (A.planned): every block derives the same plan from the device counts
+    // -- query blocks per problem, one split count sp_all for the batch that brings the items to
+    // about BF_TARGET, items (problem, query block, split) in that order -- and the blocks loop
+    // over the items; block 0 publishes the item prefix for the merge.  Otherwise one item per
+    // block from the capacities (blockIdx -> split, query block, problem).
+    int total = gridDim.x, sp_all = 1;
+    if (A.planned) {
+        const int B = A.B, per_t = (B + 255) / 256, lo = min(B, tid * per_t), hi = min(B, lo + per_t);
+        int my_qb = 0;
+        for (int b = lo; b < hi; ++b) my_qb += bf_plan(A.nq[b], A.nt[b], 1, TT).nqb;
+        int tot_qb;
+        block_scan_i32(my_qb, scan_s, &tot_qb);
+        sp_all = tot_qb > 0 ? min(BF_MAXSPLIT, max(1, (BF_TARGET + tot_qb - 1) / tot_qb)) : 1;
+        int my_items = 0;
+        for (int b = lo; b < hi; ++b) {
+            const BfPlan p = bf_plan(A.nq[b], A.nt[b], sp_all, TT);
+            my_items += p.nqb * p.sp;
+        }
+        int run = block_scan_i32(my_items, scan_s, &total);
+        for (int b = lo; b < hi; ++b) {
+            pref_s[b] = run;
+            const BfPlan p = bf_plan(A.nq[b], A.nt[b], sp_all, TT);
+            run += p.nqb * p.sp;
+        }
+        if (tid == 0) pref_s[B] = total;
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            for (int b = tid; b <= B; b += 256) A.plan[b] = pref_s[b];
+            if (tid == 0) A.plan[B + 1] = sp_all;
+        }
+    }
+    for (int item = blockIdx.x; item < total; item += gridDim.x) {      // block-uniform loop
+    int b, qb, sp, per;
+    int64_t prow;                                 // partial-result row of query q0 of this item
+    if (A.planned) {
+        int l = 0, h = A.B;                       // pref_s[l] <= item < pref_s[l + 1]
+        while (h - l > 1) {
+            const int m = (l + h) >> 1;
+            if (pref_s[m] <= item) l = m; else h = m;
+        }
+        b = l;
+        const BfPlan p = bf_plan(A.nq[b], A.nt[b], sp_all, TT);
+        const int local = item - pref_s[b];
+        qb = local / p.sp;
+        sp = local - qb * p.sp;
+        per = p.per;
+        prow = (int64_t)item * BF_QB;
+    } else {
+        const int nqb = (A.qcap + A.qb - 1) / A.qb;
+        int blk = item;
+        sp = blk % A.tsplit;
+        blk /= A.tsplit;
+        qb = blk % nqb;
+        b = blk / nqb;
+        if (b >= A.B) continue;
+        per = bf_per(A.nt[b], A);
+        prow = ((int64_t)b * A.tsplit + sp) * A.qcap + (int64_t)qb * A.qb;
+    }
     const int nq = A.nq[b], nt = A.nt[b];
     const int q0 = qb * A.qb;
-    if (q0 >= nq) return;
-    const int per = bf_per(nt, A);
+    if (q0 >= nq) continue;
     const int tlo = sp * per, thi = min(nt, tlo + per);
     const int ntile = thi > tlo ? (thi - tlo + TT - 1) / TT : 0;
-    const int tid = threadIdx.x, w = wave_id(), lane = lane_id();
     const int h = lane >> 5, col = lane & 31;
     const int8_t* qi8 = reinterpret_cast<const int8_t*>(A.qbf);
     v4i qf[QG][4];
@@ -454,8 +534,10 @@ __global__ void __launch_bounds__(256) k_bf_i8(BfArgs A)
         int j0 = i0[g], j1 = i1[g];
         merge2(d0, j0, d1, j1, __shfl_xor(d0, 32, 64), __shfl_xor(j0, 32, 64), __shfl_xor(d1, 32, 64),
                __shfl_xor(j1, 32, 64));
-        if (h == 0 && qi < nq) A.part[((int64_t)b * A.tsplit + sp) * A.qcap + qi] = make_int4(d0, j0, d1, j1);
+        if (h == 0 && qi < nq) A.part[prow + (qi - q0)] = make_int4(d0, j0, d1, j1);
     }
+    __syncthreads();                              // the next item restages the LDS tiles
+    }                                             // items
 }
 
 __global__ void __launch_bounds__(256) k_bf_merge(BfArgs A)
@@ -471,11 +553,22 @@ __global__ void __launch_bounds__(256) k_bf_merge(BfArgs A)
         return;
     }
     int d0 = INT_MAX, d1 = INT_MAX, i0 = -1, i1 = -1;
-    const int per = bf_per(A.nt[b], A);
-    for (int sp = 0; sp < A.tsplit; ++sp) {
-        if (sp * per >= A.nt[b]) break;            // empty split: its block never ran
-        const int4 p = A.part[((int64_t)b * A.tsplit + sp) * A.qcap + q];
-        merge2(d0, i0, d1, i1, p.x, p.y, p.z, p.w);
+    if (A.planned) {
+        // the items of (b, q's query block) are consecutive, one per split (k_bf_i8's plan)
+        const BfPlan p = bf_plan(A.nq[b], A.nt[b], A.plan[A.B + 1], A.tt);
+        const int qb = q / BF_QB;
+        const int64_t it0 = A.plan[b] + (int64_t)qb * p.sp;
+        for (int sp = 0; sp < p.sp; ++sp) {
+            const int4 v = A.part[(it0 + sp) * BF_QB + (q - qb * BF_QB)];
+            merge2(d0, i0, d1, i1, v.x, v.y, v.z, v.w);
+        }
+    } else {
+        const int per = bf_per(A.nt[b], A);
+        for (int sp = 0; sp < A.tsplit; ++sp) {
+            if (sp * per >= A.nt[b]) break;            // empty split: its block never ran
+            const int4 p = A.part[((int64_t)b * A.tsplit + sp) * A.qcap + q];
+            merge2(d0, i0, d1, i1, p.x, p.y, p.z, p.w);
+        }
     }
     const int qn = A.qn[(int64_t)b * A.qcap + q];
     int32_t* ix = A.idx2 + ((int64_t)b * A.qcap + q) * 2;
@@ -553,12 +646,23 @@ static int bf_tsplit_max(int B, int qcap, int tcap) { return bf_tsplit(B, qcap, 
 
 static int64_t align256(int64_t v) { return (v + 255) & ~(int64_t)255; }
 
+// partial-result rows: the capacity plan's [B][tsplit][qcap], or the device plan's items x 128
+// (items <= max(B x query blocks, 2 x BF_TARGET): one split when the query blocks alone reach the
+// target, otherwise at most target + query blocks)
+static int64_t bf_part_rows(int B, int qcap, int tcap)
+{
+    const int64_t cap_rows = (int64_t)B * bf_tsplit_max(B, qcap, tcap) * qcap;
+    const int64_t nqb = (qcap + BF_QB - 1) / BF_QB;
+    const int64_t items = (int64_t)B * nqb > 2 * BF_TARGET ? (int64_t)B * nqb : 2 * BF_TARGET;
+    return cap_rows > items * BF_QB ? cap_rows : items * BF_QB;
+}
+
 extern "C" int64_t vo_bf_knn2_batch_scratch(int B, int32_t qcap, int32_t tcap)
 {
     if (B < 1 || qcap < 1 || tcap < 1) return -1;
-    const int sp = bf_tsplit_max(B, qcap, tcap);
     return align256((int64_t)B * qcap * 256) + align256((int64_t)B * tcap * 256) + align256((int64_t)B * qcap * 4) +
-           align256((int64_t)B * tcap * 4) + align256((int64_t)B * sp * qcap * 16) + 256 + align256((int64_t)B * qcap * 4);
+           align256((int64_t)B * tcap * 4) + align256(bf_part_rows(B, qcap, tcap) * 16) + 256 +
+           align256((int64_t)B * qcap * 4) + align256((int64_t)(B + 2) * 4);
 }
 
 extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_t qcap, const float* t,
@@ -581,16 +685,26 @@ extern "C" int vo_bf_knn2_batch(int B, const float* q, const int32_t* nq, int32_
     A.tbf = (const __bf16*)p; p += align256((int64_t)B * tcap * 256);
     A.qn = (const int32_t*)p; p += align256((int64_t)B * qcap * 4);
     A.tn = (const int32_t*)p; p += align256((int64_t)B * tcap * 4);
-    A.part = (int4*)p; p += align256((int64_t)B * A.tsplit * qcap * 16);
+    A.part = (int4*)p; p += align256(bf_part_rows(B, qcap, tcap) * 16);
     A.flag_n = (int32_t*)p; p += 256;
-    A.flag_list = (int32_t*)p;
+    A.flag_list = (int32_t*)p; p += align256((int64_t)B * qcap * 4);
+    A.plan = (int32_t*)p;
     A.nq = nq; A.nt = nt; A.idx2 = idx2; A.dist2 = dist2;
     const int nqb = (qcap + A.qb - 1) / A.qb;
+    // int8 path: the device plan (splits from the real counts, not the capacities: a C3 call of 16
+    // pairs of ~1,660 descriptors in 16,384-row buffers ran 208 blocks on 256 CUs with one split);
+    // VO_BF_PLAN=0 keeps the capacity plan (A/B)
+    const char* plan_e = getenv("VO_BF_PLAN");
+    const int plan_env = plan_e ? atoi(plan_e) : 1;
+    A.planned = !use_bf16 && plan_env != 0 && B <= BF_PLAN_MAXB;
     if (!use_bf16) {
         const int qblocks = (int)(((int64_t)B * qcap + 31) / 32), tblocks = (int)(((int64_t)B * tcap + 31) / 32);
         const BfPrep Q{q, nq, qcap, (int8_t*)A.qbf, (int32_t*)A.qn}, T{t, nt, tcap, (int8_t*)A.tbf, (int32_t*)A.tn};
-        hipLaunchKernelGGL(k_bf_prep_i8, dim3(qblocks + tblocks), dim3(256), 0, st, Q, T, B, qblocks, A.flag_n);
-        hipLaunchKernelGGL((k_bf_i8<BFI_TT, 1>), dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
+        // grid-stride prep: up to 16 blocks per CU (groups past a problem's count are skipped)
+        const int pblocks = qblocks + tblocks < 4096 ? qblocks + tblocks : 4096;
+        hipLaunchKernelGGL(k_bf_prep_i8, dim3(pblocks), dim3(256), 0, st, Q, T, B, qblocks, A.flag_n);
+        if (A.planned) hipLaunchKernelGGL((k_bf_i8<BFI_TT, 1>), dim3(BF_TARGET), dim3(256), 0, st, A);
+        else hipLaunchKernelGGL((k_bf_i8<BFI_TT, 1>), dim3(B * nqb * A.tsplit), dim3(256), 0, st, A);
     } else {
         if (hipMemsetAsync(A.flag_n, 0, sizeof(int32_t), st) != hipSuccess) return VO_EHIP;
         hipLaunchKernelGGL(k_bf_prep, dim3(((int64_t)B * qcap + 3) / 4), dim3(256), 0, st, q, nq, B, qcap, 2.f,

@@ -92,6 +92,16 @@ def test_bf_knn2_batch_exact():
             assert (idx2[b, :nq, 1] == -1).all()
         big += int((ed[:, 1] >= 2048.0).sum())
     assert big > 0          # the fixup path ran
+    # the capacity plan (one item per block from the buffer sizes, VO_BF_PLAN=0) gives the same
+    # result as the default device plan (splits from the real counts)
+    import os
+    os.environ["VO_BF_PLAN"] = "0"
+    try:
+        i4, d4 = bf_knn2_batch(torch.from_numpy(q).to(dev), nq_d, torch.from_numpy(t).to(dev), nt_d)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["VO_BF_PLAN"]
+    assert np.array_equal(i4.cpu().numpy(), idx2) and np.array_equal(d4.cpu().numpy(), dist2)
     # a caller-owned scratch buffer (what an Engine passes) gives the same result
     scr = torch.empty(matcher_scratch_bytes(B, qcap, tcap), dtype=torch.uint8, device=dev)
     i3, d3 = bf_knn2_batch(torch.from_numpy(q).to(dev), nq_d, torch.from_numpy(t).to(dev), nt_d, scratch=scr)
