@@ -52,6 +52,7 @@ from monocular_visual_odometry_va4mr_amd.synth import Renderer, poses  # noqa: E
 from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E402
 
 SEQ_LEN = 4541          # KITTI seq00 frame count
+SEQ_OVERLAP = 30        # frames shared by neighbouring shards of the sequence job (--seq-overlap)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
 MFMA_PEAK_TF = 2500.0   # dense bf16 MFMA (no sparsity)
 MFMA_PEAK_I8 = 5000.0   # dense int8 MFMA: 32x32x32 in the cycles of bf16 32x32x16 (MI355X_MICROARCH.md)
@@ -83,6 +84,9 @@ def parse():
                     help="shards per GPU of the whole-sequence job (n_shards = world x this; default "
                          "seq_chains_for(world))")
     ap.add_argument("--seq-groups", type=int, default=None, help="stream groups of the sequence job")
+    ap.add_argument("--seq-overlap", type=int, default=SEQ_OVERLAP,
+                    help="frames shared by neighbouring shards of the sequence job (reference fixtures: "
+                         "tests/golden/kitti_seq00_shards*.npz)")
     ap.add_argument("--no-rank-slices", action="store_true",
                     help="skip the one-rank-of-N sequence slices (rank 0 of world 2 / 4 / 8 on this GPU)")
     # hardware queues: the package sets GPU_MAX_HW_QUEUES=8 at import unless the environment
@@ -301,9 +305,9 @@ def seq_chains_for(world: int) -> int:
     return 64 if world <= 1 else 32
 
 
-def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3):
+def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3, overlap=SEQ_OVERLAP):
     """The whole C2 sequence as one job: SEQ_LEN frames cut into
-    world x per_gpu overlapping shards (30-frame overlap), per_gpu chains on every rank (the
+    world x per_gpu overlapping shards (`overlap` frames shared), per_gpu chains on every rank (the
     shards per GPU are the batch dimension, main.py:166-175's loop split across chains),
     bootstrap included in the clock (frames pre-rendered into HBM), poses gathered to rank 0
     and stitched.  frames/s = SEQ_LEN unique frames / wall.  Every shard's trajectory is
@@ -312,15 +316,13 @@ def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3):
     truth.  Run `reps` times; the median run (by wall) is reported and every run's wall is
     listed (`wall_s_runs`, in run order; the first pays one-time costs).
     Wall-time model: bootstrap(B) + n_steps x step(B), n_steps = ceil(SEQ_LEN /
-    shards) + 30 - 3: the 30-frame overlap caps the job once SEQ_LEN / shards approaches it."""
-    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
+    shards) + overlap - 3: the overlap caps the job once SEQ_LEN / shards approaches it."""
+    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_for, run
     n_shards = world * per_gpu
-    ref = None
-    for name in ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz"):
-        ref = ref or reference_shards(os.path.join(ROOT, "tests", "golden", name), n_shards)
+    ref = reference_for(os.path.join(ROOT, "tests", "golden"), n_shards, overlap)
     runs = []
     for _ in range(reps):
-        r = run("kitti", SEQ_LEN, per_gpu, overlap=30, seed=seed, device=device, rank=rank, world=world,
+        r = run("kitti", SEQ_LEN, per_gpu, overlap=overlap, seed=seed, device=device, rank=rank, world=world,
                 reference=ref, time_boot=False, groups=groups)
         if r is not None:
             runs.append(r)
@@ -330,7 +332,7 @@ def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3):
     res = sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2]
     st = res.get("stitched") or {}
     vs = res.get("vs_reference")
-    return {"config": f"C2 whole sequence: {SEQ_LEN} frames as {res['shards']} overlapping shards "
+    return {"overlap": overlap, "config": f"C2 whole sequence: {SEQ_LEN} frames as {res['shards']} overlapping shards "
                       f"({per_gpu} per GPU, {res['groups']} stream group(s)) on {world} GPU(s), "
                       "bootstrap + every step timed, poses gathered + Sim(3)-stitched after",
             "frames_per_s": res["sequence_frames_per_s"], "wall_s": res["wall_s"], "reported": f"median of {len(runs)} runs",
@@ -347,7 +349,7 @@ def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3):
             "stitched_ate_rel_vs_gt": st.get("ate_rel")}
 
 
-def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3):
+def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3, overlap=SEQ_OVERLAP):
     """What one rank of an N-GPU sequence job does, measured on this GPU:
     rank 0's slice of the world = N plan (N x seq_chains_for(N) shards of the C2 sequence; for
     N = 8, shards 0..31 of the 256-shard cut) run alone, bootstrap included, every shard
@@ -356,22 +358,20 @@ def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3):
     rank's wall; `..._incl_stitch` adds the batched stitch of all N x B shards (timed on the
     reference cut's own poses) -- the RCCL gather of ~0.4 MB is not modelled.  Median of `reps`
     runs per N, every run's wall listed."""
-    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
+    from monocular_visual_odometry_va4mr_amd.run_sequence import reference_for, run
     out = {}
     for world in worlds:
         per_gpu = seq_chains_for(world)
         n_shards = world * per_gpu
-        ref = None
-        for name in ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz"):
-            ref = ref or reference_shards(os.path.join(ROOT, "tests", "golden", name), n_shards)
+        ref = reference_for(os.path.join(ROOT, "tests", "golden"), n_shards, overlap)
         runs = []
         for _ in range(reps):
-            r = run("kitti", SEQ_LEN, per_gpu, overlap=30, seed=seed, device=device, rank=0, world=world,
+            r = run("kitti", SEQ_LEN, per_gpu, overlap=overlap, seed=seed, device=device, rank=0, world=world,
                     reference=ref, time_boot=False)
             runs.append(r)
             torch.cuda.empty_cache()
         res = sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2]
-        stitch_ms = stitch_time_ms(ref, n_shards) if ref else None
+        stitch_ms = stitch_time_ms(ref, n_shards, overlap) if ref else None
         vs = res.get("vs_reference") or {}
         out[str(world)] = {
             "shards_total": n_shards, "rank0_shards": res["shards"], "groups": res["groups"],
@@ -387,10 +387,10 @@ def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3):
     return out
 
 
-def stitch_time_ms(ref: dict, n_shards: int, iters: int = 5) -> float:
+def stitch_time_ms(ref: dict, n_shards: int, overlap: int = 30, iters: int = 5) -> float:
     """Median wall of shards.stitch over the reference cut's own per-shard positions (the
     input rank 0 stitches after the gather, at the job's full shard count)."""
-    plan = Sh.plan_shards(SEQ_LEN, n_shards, 2, 30)
+    plan = Sh.plan_shards(SEQ_LEN, n_shards, 2, overlap)
     cs = [ref[k] for k in range(n_shards)]
     ts = []
     for _ in range(iters):
@@ -665,12 +665,12 @@ def main():
     if not args.no_sequence:
         try:                          # a secondary measurement never costs the headline line
             seq = sequence_leg(device, args.seed, rank, world, per_gpu=args.seq_chains or seq_chains_for(world),
-                               groups=args.seq_groups)
+                               groups=args.seq_groups, overlap=args.seq_overlap)
         except Exception as exc:  # noqa: BLE001
             seq = {"error": f"{type(exc).__name__}: {exc}"}
         if world == 1 and not args.no_rank_slices and "error" not in (seq or {}):
             try:
-                seq["rank_slices"] = rank_slice_leg(device, args.seed)
+                seq["rank_slices"] = rank_slice_leg(device, args.seed, overlap=args.seq_overlap)
             except Exception as exc:  # noqa: BLE001
                 seq["rank_slices"] = {"error": f"{type(exc).__name__}: {exc}"}
 

@@ -376,13 +376,6 @@ VO_DEV __amdgpu_buffer_rsrc_t lkq_rsrc(const void* base, int64_t bytes)
 #ifndef LK_JPRE
 #define LK_JPRE 1
 #endif
-// k_lk_w's I window: packed 2x2 quads (default) or the byte rows of round 4 (VO_LK_TENSOR_BYTES,
-// and the VO_LK_TENSOR_BATCH diagnostics build, which reads the bytes)
-#if defined(VO_LK_TENSOR_BYTES) || defined(VO_LK_TENSOR_BATCH) || defined(VO_LKX_NOSTAGE)
-#define LK_I_BYTES 1
-#else
-#define LK_I_BYTES 0
-#endif
 VO_DEV void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -654,7 +647,7 @@ __device__ long long g_lkprof[VO_MAX_LEVELS][1024][8];
 // caller must leave after each pyramid -- launch_lk checks it).  Arithmetic is identical to
 // k_lk (bit-exact with the CPU restatement).
 template <int WW, int WH>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd, int boff)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) k_lk_w(LKParams P, int level_hi, int level_lo, int B, int nb, int xcd)
 {
     constexpr int WPB = 1;
     constexpr int NPX = WW * WH, MAXJ = (NPX + 63) / 64;
@@ -669,25 +662,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                   "k_lk_w staging layout");
     // one spare row in QT / IR / DR: read (never used) by the dead lanes of window row 15
     __shared__ uint4 QT4_all[WPB][(TH + 1) * QM];
-#if LK_I_BYTES
     __shared__ uint32_t IR_all[WPB][(WH + 2) * IRS];
-#else
-    // the I window as packed 2x2 quads like QT (round 5): one ds_read_b32 +
-    // two v_dot4 per tap instead of four ds_read_u8 + four multiplies; 16 quad rows of 16
-    __shared__ uint4 QI4_all[WPB][16 * 4];
-#endif
     __shared__ uint32_t DR_all[WPB][(WH + 2) * QS];
     const int wv = WPB > 1 ? (int)(threadIdx.x >> 6) : 0;
     uint4* QT4 = QT4_all[wv];
     const uint32_t* QT = reinterpret_cast<const uint32_t*>(QT4);
-#if LK_I_BYTES
     uint32_t* IR = IR_all[wv];
-    const uint8_t* ir8 = (const uint8_t*)IR;
-#else
-    uint4* QI4 = QI4_all[wv];
-    const uint32_t* QI = reinterpret_cast<const uint32_t*>(QI4);
-#endif
     uint32_t* DR = DR_all[wv];
+    const uint8_t* ir8 = (const uint8_t*)IR;
     int b, pb, pcur = -1;
     const int lane = lane_id();
     int level = level_lo;
@@ -695,7 +677,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     for (level = level_hi; level >= level_lo; --level)
         for (int k = 2; k < 8; ++k) LKPROF_SET(k, 0);
     level = level_lo;
-    if (!lk_block(B, nb, b, pb, xcd != 0, (boff + (int)blockIdx.x) * WPB + wv)) return;
+    if (!lk_block(B, nb, b, pb, xcd != 0, (int)blockIdx.x * WPB + wv)) return;
     if (P.chain_status && P.chain_status[b] != 0) return;
     const int n0 = P.n0 ? P.n0[b] : 0;
     int n1 = P.n1 ? P.n1[b] : 0;
@@ -715,9 +697,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     const int toff0 = wrow * QS + wcol;
     int toff[MAXJ];
     bool live[MAXJ];
-#if !LK_I_BYTES
-    const int toffq = wrow * 16 + wcol;              // QI: quad (wrow + 4 j, wcol) at toffq + 64 j
-#endif
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
         live[j] = wcol < WW && wrow + 4 * j < WH;
@@ -732,7 +711,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     // and store (LDS writes), so that every load of a stage is in flight at once: one memory
     // round trip per stage instead of one per loop trip.
     constexpr int NIR = ((WH + 1) * 8 + 63) / 64, NDR = ((WH + 1) * 16 + 63) / 64;
-    (void)NIR;
     constexpr int NJR = (TH * JRS + 63) / 64;             // 8 quad rows per load round
     // J tile origin covering the window at (inx, iny)
     auto j_origin = [&](int inx, int iny) {
@@ -854,9 +832,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // of DR below is conflict-free (rows r, r + 1 at QS = 24 collided 2-way)
                 const int drow = 2 * ((ln >> 4) & 1) + (ln >> 5);
                 const int vd = 4 * (loff + gy * pitch + gx + drow * pitch + (ln & 15));
-                uint32_t vdd[NDR], vjr[2][NJR];
-#if LK_I_BYTES
-                uint32_t vir[NIR];
+                uint32_t vir[NIR], vdd[NDR], vjr[2][NJR];
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
                     LKCHKO(vi + 8 * k * pitch, P.pstride, "I");
@@ -866,18 +842,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     vir[k] = __builtin_amdgcn_raw_buffer_load_b32(rI, vi, 8 * k * pitch, 0);
 #endif
                 }
-#else
-                // I quads: lane -> quad row ln >> 2 (0..15), columns 4 (ln & 3) .. + 3, from the
-                // aligned dwords m, m + 1 of I rows r and r + 1 (the window's bytes start at ish)
-                (void)vi;
-                const int vq = loff + gy * pitch + (gx & ~3) + (ln >> 2) * pitch + 4 * (ln & 3);
-                uint32_t viq[4];
-                LKCHKO(vq + pitch + 4, P.pstride, "I");
-                viq[0] = __builtin_amdgcn_raw_buffer_load_b32(rI, vq, 0, 0);
-                viq[1] = __builtin_amdgcn_raw_buffer_load_b32(rI, vq, 4, 0);
-                viq[2] = __builtin_amdgcn_raw_buffer_load_b32(rI, vq, pitch, 0);
-                viq[3] = __builtin_amdgcn_raw_buffer_load_b32(rI, vq, pitch + 4, 0);
-#endif
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
                     LKCHKO(vd + 16 * k * pitch, 2 * P.dstride, "D");
@@ -897,26 +861,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     }
                 }
                 wave_lds_sync();
-#if LK_I_BYTES
 #pragma unroll
                 for (int k = 0; k < NIR; ++k) {
                     const int r = (ln >> 3) + 8 * k, c = ln & 7;
                     if (c < IRS) IR[r * IRS + c] = vir[k];
                 }
-#else
-                {
-                    // quad byte order (I[r][c], I[r][c+1], I[r+1][c], I[r+1][c+1]), as j_store
-                    const uint32_t a0 = viq[0], a1 = viq[1], b0 = viq[2], b1 = viq[3];
-                    const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, ish);
-                    const uint32_t Bv = ish == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, ish + 1);
-                    const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, ish);
-                    const uint32_t D = ish == 3 ? b1 : __builtin_amdgcn_alignbyte(b1, b0, ish + 1);
-                    const uint32_t X = __builtin_amdgcn_perm(Bv, A, 0x05010400u), Y = __builtin_amdgcn_perm(Bv, A, 0x07030602u);
-                    const uint32_t Xp = __builtin_amdgcn_perm(D, C, 0x05010400u), Yp = __builtin_amdgcn_perm(D, C, 0x07030602u);
-                    QI4[ln] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
-                                         __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
-                }
-#endif
 #pragma unroll
                 for (int k = 0; k < NDR; ++k) {
                     const int r = drow + 4 * k, c = ln & 15;
@@ -941,11 +890,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // per sum (exact: |dI| <= 4080, weights <= 2^14)
                 const v2i16 wp0 = as_v2i16((uint32_t)(iw00 & 0xffff) | ((uint32_t)iw01 << 16));
                 const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
-#if !LK_I_BYTES
-                const int ineg = iw11 < 0;
-                const uint32_t iwlo = pack_w(iw00, iw01, iw10, iw11 + ineg, 0, 127);
-                const uint32_t iwhi = pack_w(iw00, iw01, iw10, iw11 + ineg, 7, 255);
-#endif
 #ifdef VO_LK_TENSOR_BATCH
                 // diagnostics build (the round-4 variant that was dropped): the
                 // level's 24 tensor LDS reads issued together ahead of a scheduling barrier
@@ -969,21 +913,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     const uint32_t d00 = tdq[j][0], d01 = tdq[j][1], d10 = tdq[j][2], d11 = tdq[j][3];
                     const int v = DESCALE(__mul24(tsv[j][0], iw00) + __mul24(tsv[j][1], iw01) +
                                           __mul24(tsv[j][2], iw10) + __mul24(tsv[j][3], iw11), 9);
-#elif LK_I_BYTES
+#else
                     const uint8_t* s = ir8 + toff[j] + ish;
                     const uint32_t* d = DR + toff[j];
                     const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
                     const int v = DESCALE(__mul24((int)s[0], iw00) + __mul24((int)s[1], iw01) +
                                           __mul24((int)s[QS], iw10) + __mul24((int)s[QS + 1], iw11), 9);
-#else
-                    const uint32_t* d = DR + toff[j];
-                    const uint32_t d00 = d[0], d01 = d[1], d10 = d[QS], d11 = d[QS + 1];
-                    // DESCALE(sum I w, 9) as two v_dot4 on the 7 + 7-bit weight split (iw11 = -1:
-                    // dot with 0 and subtract the tap once), as the iterations form J
-                    const uint32_t q = QI[toffq + 64 * j];
-                    uint32_t isum = (__builtin_amdgcn_udot4(q, iwhi, 0u, false) << 7) + __builtin_amdgcn_udot4(q, iwlo, 256u, false);
-                    if (ineg) isum -= q >> 24;
-                    const int v = (int)isum >> 9;
 #endif
                     const int gx2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x05040100u)), wp1,
                                         __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x05040100u)), wp0,
@@ -2157,16 +2092,7 @@ static int launch_lk(const LKParams& P, int B, hipStream_t st)
     // sizes (cv2.calcOpticalFlowPyrLK's default 21x21 on the cv2compat surface): k_lk, one
     // launch per level.
     if (staged15) {
-        // VO_LK_CHUNKS = n (measurement option): the grid as n launches over consecutive chain
-        // ranges; between them the stream drains, and other streams' blocks can take the freed
-        // wave slots and LDS (results identical)
-        static const int chunks_env = [] { const char* e = getenv("VO_LK_CHUNKS"); return e ? atoi(e) : 1; }();
-        const int nch = chunks_env > 1 && !xcd_env ? chunks_env : 1;
-        const int per = ((nblk / nb + nch - 1) / nch) * nb;          // whole chains per launch
-        for (int c0 = 0; c0 < nblk; c0 += per) {
-            const int n = nblk - c0 < per ? nblk - c0 : per;
-            hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(n), dim3(64), 0, st, P, L, 0, B, nb, xcd_env, c0);
-        }
+        hipLaunchKernelGGL((k_lk_w<15, 15>), dim3(nblk), dim3(64), 0, st, P, L, 0, B, nb, xcd_env);
         return hip_ok() ? VO_OK : VO_EHIP;
     }
     for (int level = P.L; level >= 0; --level) {

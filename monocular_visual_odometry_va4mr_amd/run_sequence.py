@@ -274,6 +274,29 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     return out
 
 
+def shard_fixture_paths(golden_dir: str, overlap: int = 30) -> list:
+    """The shard fixture files that hold cuts with this overlap (make_long_golden.py): 30 frames
+    in kitti_seq00_shards.npz (8, 16) and kitti_seq00_shards_wide.npz (32 .. 256); other overlaps
+    in kitti_seq00_shards_o{overlap}.npz."""
+    names = ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz") if overlap == 30 else \
+        (f"kitti_seq00_shards_o{overlap}.npz",)
+    out = []
+    for n in names:
+        p = os.path.join(golden_dir, n)
+        if os.path.exists(p) and int(np.load(p, allow_pickle=False)["overlap"]) == overlap:
+            out.append(p)
+    return out
+
+
+def reference_for(golden_dir: str, n_shards: int, overlap: int = 30) -> dict | None:
+    """Per-shard reference trajectories of the cut (n_shards, overlap), or None."""
+    for p in shard_fixture_paths(golden_dir, overlap):
+        r = reference_shards(p, n_shards)
+        if r is not None:
+            return r
+    return None
+
+
 def reference_shards(path: str, n_shards: int) -> dict | None:
     """Per-shard reference CPU trajectories from tests/golden/kitti_seq00_shards.npz
     (generated by the reference class on the same shard boundaries, make_long_golden.py)."""
