@@ -8,8 +8,9 @@ make_long_golden.py: /root/reference/VisualOdometryPipeLine.py on the oracle pri
   current fixture: "Not enough keypoints for PnP" at frame 4535, 4533 poses);
 * the sequence cut into 16 and into 8 shards (C4's layout) and into the wider cuts of the
   sequence job (32 .. 256 shards: shards per GPU as the batch dimension, run in 1 and 2 stream
-  groups) on the same boundaries as the reference runs: every shard's trajectory bit-identical
-  to its reference run, no failed shard and no coverage break in the stitched trajectory.
+  groups), with the 30-frame overlap and the sequence job's 15-frame one, on the same boundaries
+  as the reference runs: every shard's trajectory bit-identical to its reference run, no failed
+  shard and no coverage break in the stitched trajectory.
 
 Frames are rendered on the GPU and checked against the fixture's SHA-1 digests."""
 import hashlib
@@ -84,20 +85,21 @@ def test_full_sequence_matches_reference():
     assert rel == 0.0 or rel < 1e-12
 
 
-def _shard_fixture(n_shards):
-    for name in ("kitti_seq00_shards.npz", "kitti_seq00_shards_wide.npz"):
-        path = os.path.join(GOLDEN, name)
-        if os.path.exists(path):
-            g = np.load(path, allow_pickle=False)
-            if f"s{n_shards}_t" in g.files:
-                return path, {k: g[k] for k in g.files}
-    pytest.skip(f"no reference fixture for {n_shards} shards (tests/golden/make_long_golden.py --cuts)")
+def _shard_fixture(n_shards, overlap=30):
+    from monocular_visual_odometry_va4mr_amd.run_sequence import shard_fixture_paths
+    for path in shard_fixture_paths(GOLDEN, overlap):
+        g = np.load(path, allow_pickle=False)
+        if f"s{n_shards}_t" in g.files:
+            return path, {k: g[k] for k in g.files}
+    pytest.skip(f"no reference fixture for {n_shards} shards, overlap {overlap} (tests/golden/make_long_golden.py)")
 
 
-@pytest.mark.parametrize("n_shards,groups", [(16, 1), (8, 1), (32, 2), (64, 1), (64, 2), (128, 2), (256, 2)])
-def test_sharded_sequence_matches_reference_per_shard(n_shards, groups):
+@pytest.mark.parametrize("n_shards,groups,overlap", [(16, 1, 30), (8, 1, 30), (32, 2, 30), (64, 1, 30), (64, 2, 30),
+                                                     (128, 2, 30), (256, 2, 30), (64, 2, 15), (256, 2, 15)])
+def test_sharded_sequence_matches_reference_per_shard(n_shards, groups, overlap):
     from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
-    path, g = _shard_fixture(n_shards)
+    path, g = _shard_fixture(n_shards, overlap)
+    assert int(g["overlap"]) == overlap
     assert all(str(e) == "" for e in g[f"s{n_shards}_error"])
     ref = reference_shards(path, n_shards)
     # as the bench's sequence leg: the stream groups are not synchronised after their bootstraps,

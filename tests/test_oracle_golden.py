@@ -61,26 +61,29 @@ def test_golden_sanity():
 def test_wide_shard_fixtures_consistent_and_pinned():
     """The sequence job's shard fixtures (kitti_seq00_shards*.npz, make_long_golden.py --cuts):
     shard 0 of every cut bootstraps at frame 0 like the one-chain run, so its trajectory is
-    a prefix of kitti_seq00.npz; and the restatement reproduces a whole shard of the widest
-    cut (its last one, 16 poses) from frames re-rendered here and checked against the digests."""
+    a prefix of kitti_seq00.npz, and its bounds are shards.plan_shards' for its overlap (30, and
+    the sequence job's 15); and the restatement reproduces a whole shard of the widest 15-frame
+    cut (its last one) from frames re-rendered here and checked against the digests."""
     import os
     from conftest import GOLDEN
     full = load_golden("kitti_seq00")
     cuts = {}
-    for name in ("kitti_seq00_shards", "kitti_seq00_shards_wide"):
+    for name in ("kitti_seq00_shards", "kitti_seq00_shards_wide", "kitti_seq00_shards_o15"):
         if os.path.exists(os.path.join(GOLDEN, f"{name}.npz")):
             g = load_golden(name)
             for k in g:
                 if k.endswith("_t"):
-                    cuts[int(k[1:-2])] = g
-    assert {8, 16}.issubset(cuts)
-    for S, g in cuts.items():
+                    cuts[(int(k[1:-2]), int(g["overlap"]))] = g
+    assert {(8, 30), (16, 30), (256, 30), (256, 15)}.issubset(cuts)
+    from monocular_visual_odometry_va4mr_amd import shards as Sh
+    for (S, O), g in cuts.items():
         t, off = g[f"s{S}_t"], g[f"s{S}_off"]
         assert len(off) == S + 1 and off[-1] == len(t)
         assert all(str(e) == "" for e in g[f"s{S}_error"])
-        assert np.array_equal(t[off[0]:off[1]], full["t"][:off[1] - off[0]]), f"cut {S}: shard 0 is not the chain's prefix"
-    S = max(cuts)
-    g = cuts[S]
+        assert np.array_equal(g[f"s{S}_bounds"], [[s.start, s.boot1, s.end] for s in Sh.plan_shards(4541, S, 2, O)])
+        assert np.array_equal(t[off[0]:off[1]], full["t"][:off[1] - off[0]]), f"cut {S}/{O}: shard 0 is not the chain's prefix"
+    S = 256
+    g = cuts[(S, 15)]
     start, boot1, end = (int(v) for v in g[f"s{S}_bounds"][-1])
     import hashlib
     import torch
