@@ -40,6 +40,7 @@ def main():
         print(json.dumps({"world": world, "per_gpu": B, "overlap": O, "groups": r["groups"], "wall_s": r["wall_s"],
                           "wall_s_runs": [x["wall_s"] for x in runs], "bootstrap_s": r["bootstrap_s"],
                           "steps": r["steps"], "ms_per_step": round(r["step_s"] / max(1, r["steps"]) * 1e3, 4),
+                          "host_launch_s": r["host_launch_s"],
                           "predicted_frames_per_s": round(4541 / r["wall_s"], 1), "shards_ok": r["shards_ok"],
                           "shards_compared": vs.get("shards_compared"), "shards_identical": vs.get("shards_identical")}),
               flush=True)
