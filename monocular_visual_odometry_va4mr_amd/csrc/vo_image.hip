@@ -272,6 +272,212 @@ __global__ void __launch_bounds__(256) k_pyr01(PyrLevelArgs A0, PyrLevelArgs A1,
     }
 }
 
+// k_pyr_rows<L0>: one pyramid level and its Scharr derivatives, streamed down the rows by
+// single waves without LDS (round 5).  pyr_tile's blocks hold four wave slots and 25 KB of
+// LDS each, so while another stream group's LK waves fill the CUs they wait for a CU to drain;
+// a block of this kernel fits in the slot one finished LK wave frees.  A wave owns R level
+// rows of a strip of 64 x 4 padded columns (lane = 4 consecutive columns; lanes 0 and 63 are
+// halo lanes that only feed their neighbours' Scharr taps; strips step by PR_STEP columns and
+// the last one is right-aligned, so it alone writes the right border):
+//   level 0  row y is frame row y: two aligned dword loads and a byte align per lane (buffer
+//            loads: a row end never reads past the frame buffer);
+//   pyrDown  the horizontal [1 4 6 4 1] of source rows 2y-2 .. 2y+2 as packed u16 pairs (8
+//            aligned source bytes per lane, the two outer taps from the neighbour lanes by DPP
+//            wave shifts), kept in a five-row ring that advances two source rows per level
+//            row, then the vertical taps and (acc + 128) >> 8 -- pyr_tile's integers exactly.
+// Reflect-101 columns take their mirror column's byte by ds_bpermute inside the strip; the
+// mirrored border rows are written by the wave that computes their source row; the Scharr of
+// row y reads rows y-1, y, y+1 (the chunk's two halo rows evaluated on their own, reflect-101
+// at the level's first and last row).  Same bytes and derivatives as pyr_tile.
+#define PR_STEP 248
+template <bool L0>
+__global__ void __launch_bounds__(64) k_pyr_rows(PyrLevelArgs A, int R)
+{
+    const int lane = threadIdx.x;
+    const int b = blockIdx.z;
+    const int wo = A.w, ho = A.h;
+    const int pw = wo + 2 * VO_BORDER, ph = ho + 2 * VO_BORDER;
+    const int pwa = (pw + 3) & ~3;
+    const int ns = (pwa + PR_STEP - 1) / PR_STEP;
+    const bool lastst = (int)blockIdx.x == ns - 1;
+    const int base = lastst ? max(pwa - 252, -4) : (int)blockIdx.x * PR_STEP - 4;
+    const int px = base + 4 * lane;
+    const int y0 = (int)blockIdx.y * R;
+    if (y0 >= ho || (int)blockIdx.x >= ns) return;
+    const int y1 = min(y0 + R, ho);
+    // columns this wave writes: [lo, hi); the earlier strips stop short of the last one's range,
+    // so a border column and the Scharr taps next to it come from one wave only
+    const int lo = lastst ? max(pwa - PR_STEP, 0) : (int)blockIdx.x * PR_STEP;
+    const int hi = lastst ? pwa : min((int)blockIdx.x * PR_STEP + PR_STEP, pwa - PR_STEP);
+    const bool wlane = lane >= 1 && lane <= 62 && px >= lo && px < hi && px < pw;
+    const bool dlane = wlane && px + 3 >= VO_BORDER && px < VO_BORDER + wo;
+    // per byte of the lane: the strip position (lane * 4 + byte) holding its value
+    int fsrc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = px + j;
+        const int sp = (c >= 0 && c < pw) ? VO_BORDER + refl101(c - VO_BORDER, wo) : c;
+        const int rel = sp - base;
+        fsrc[j] = (rel >= 0 && rel < 256) ? rel : 4 * lane + j;
+    }
+    const bool fixcols = base < VO_BORDER || base + 256 > VO_BORDER + wo;   // wave-uniform
+    auto fix = [&](uint32_t v) -> uint32_t {
+        if (!fixcols) return v;
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute((fsrc[j] >> 2) << 2, (int)v);
+            o |= ((t >> (8 * (fsrc[j] & 3))) & 0xffu) << (8 * j);
+        }
+        return o;
+    };
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A.src + (int64_t)b * A.sstride), (short)0, (int)A.sstride, 0x00020000);
+    uint8_t* dst = A.pyr + (int64_t)b * A.pstride + A.off;
+    // write level row y (+ the border rows that mirror it)
+    auto put_row = [&](int y, uint32_t v) {
+        if (!wlane) return;
+        *(uint32_t*)(dst + (int64_t)(VO_BORDER + y) * A.pitch + px) = v;
+        if (ho >= VO_BORDER + 2) {
+            if (y >= 1 && y <= VO_BORDER) *(uint32_t*)(dst + (int64_t)(VO_BORDER - y) * A.pitch + px) = v;
+            if (y >= ho - 1 - VO_BORDER && y <= ho - 2)
+                *(uint32_t*)(dst + (int64_t)(VO_BORDER + 2 * ho - 2 - y) * A.pitch + px) = v;
+        } else {
+            for (int py = 0; py < ph; ++py) {
+                if (py == VO_BORDER) py = VO_BORDER + ho;
+                if (py < ph && refl101(py - VO_BORDER, ho) == y) *(uint32_t*)(dst + (int64_t)py * A.pitch + px) = v;
+            }
+        }
+    };
+    // Scharr of level row y from rows u = y-1, c = y, l = y+1 (calcSharrDeriv, as pyr_tile)
+    auto put_der = [&](int y, uint32_t u, uint32_t c, uint32_t l) {
+        const uint32_t ul = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x138, 0xF, 0xF, false);   // lane - 1
+        const uint32_t cl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x138, 0xF, 0xF, false);
+        const uint32_t ll = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l, 0x138, 0xF, 0xF, false);
+        const uint32_t ur = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x130, 0xF, 0xF, false);   // lane + 1
+        const uint32_t cr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x130, 0xF, 0xF, false);
+        const uint32_t lr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)l, 0x130, 0xF, 0xF, false);
+        if (!dlane || !A.der) return;
+        const uint64_t U5 = ((uint64_t)u << 8) | (ul >> 24) | ((uint64_t)(ur & 0xff) << 40);
+        const uint64_t L5 = ((uint64_t)l << 8) | (ll >> 24) | ((uint64_t)(lr & 0xff) << 40);
+        const uint64_t C5 = ((uint64_t)c << 8) | (cl >> 24) | ((uint64_t)(cr & 0xff) << 40);
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int dx = 0, dy = 0;
+            const int x = px + i - VO_BORDER;
+            if (x >= 0 && x < wo) {
+                const int uL = (int)((U5 >> (8 * i)) & 0xff), uc = (int)((U5 >> (8 * i + 8)) & 0xff),
+                          uR = (int)((U5 >> (8 * i + 16)) & 0xff);
+                const int lL = (int)((L5 >> (8 * i)) & 0xff), lc = (int)((L5 >> (8 * i + 8)) & 0xff),
+                          lR = (int)((L5 >> (8 * i + 16)) & 0xff);
+                const int cL = (int)((C5 >> (8 * i)) & 0xff), cR = (int)((C5 >> (8 * i + 16)) & 0xff);
+                dx = ((uR + lR) * 3 + cR * 10) - ((uL + lL) * 3 + cL * 10);
+                dy = ((lR - uR) + (lL - uL)) * 3 + (lc - uc) * 10;
+            }
+            o[i] = (uint32_t)(uint16_t)(int16_t)dx | ((uint32_t)(uint16_t)(int16_t)dy << 16);
+        }
+        int16_t* dq = A.der + (int64_t)b * A.dstride + 2 * (A.off + (int64_t)(VO_BORDER + y) * A.pitch + px);
+        *(uint4*)dq = make_uint4(o[0], o[1], o[2], o[3]);
+    };
+    if constexpr (L0) {
+        // frame row y: bytes px - B .. px - B + 3 (byte align shift uniform over the wave)
+        auto ld_row = [&](int y, uint32_t& d0, uint32_t& d1) {
+            const int ro = y * wo + base - VO_BORDER;
+            const int al = (ro & ~3) + 4 * lane;
+            d0 = __builtin_amdgcn_raw_buffer_load_b32(rs, al, 0, 0);
+            d1 = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 4, 0, 0);
+        };
+        auto val = [&](int y, uint32_t d0, uint32_t d1) {
+            return fix(__builtin_amdgcn_alignbyte(d1, d0, (uint32_t)((y * wo + base - VO_BORDER) & 3)));
+        };
+        uint32_t a0, a1, c0, c1, n0, n1;
+        const int yh = refl101(y0 - 1, ho);
+        ld_row(yh, a0, a1);
+        ld_row(y0, c0, c1);
+        ld_row(y0 + 1 < y1 ? y0 + 1 : refl101(y1, ho), n0, n1);
+        uint32_t vu = val(yh, a0, a1);
+        uint32_t vc = val(y0, c0, c1);
+        put_row(y0, vc);
+        for (int y = y0; y < y1; ++y) {
+            const int yn = y + 1 < y1 ? y + 1 : refl101(y1, ho);
+            const uint32_t vl = val(yn, n0, n1);
+            // the row after next, in flight while this row's Scharr runs
+            const int y2 = y + 2 < y1 ? y + 2 : refl101(y1, ho);
+            if (y + 1 < y1) ld_row(y2, n0, n1);
+            if (y + 1 < y1) put_row(y + 1, vl);
+            put_der(y, vu, vc, vl);
+            vu = vc;
+            vc = vl;
+        }
+    } else {
+        const int loff = 2 * px - VO_BORDER;              // 8-aligned source column of byte 0
+        auto ld_src = [&](int sr, uint32_t& d0, uint32_t& d1) {
+            const int o = (int)A.soff + (VO_BORDER + sr) * A.spitch + loff;
+            d0 = __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, 0);
+            d1 = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4, 0, 0);
+        };
+        constexpr uint32_t K4 = 0x04060401u;               // taps 1, 4, 6, 4 (+ the fifth)
+        auto hsum = [&](uint32_t D0, uint32_t D1, uint32_t& h01, uint32_t& h23) {
+            const uint32_t L1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D1, 0x138, 0xF, 0xF, false);   // lane - 1
+            const uint32_t R0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)D0, 0x130, 0xF, 0xF, false);   // lane + 1
+            const uint32_t o0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D0, L1, 2), K4, (D0 >> 16) & 0xffu, false);
+            const uint32_t o1 = __builtin_amdgcn_udot4(D0, K4, D1 & 0xffu, false);
+            const uint32_t o2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(D1, D0, 2), K4, (D1 >> 16) & 0xffu, false);
+            const uint32_t o3 = __builtin_amdgcn_udot4(D1, K4, R0 & 0xffu, false);
+            h01 = o0 | (o1 << 16);
+            h23 = o2 | (o3 << 16);
+        };
+        auto vert = [&](const uint32_t (&hx)[5], const uint32_t (&hy)[5]) {
+            const uint32_t ax = hx[0] + 4 * hx[1] + 6 * hx[2] + 4 * hx[3] + hx[4] + 0x00800080u;
+            const uint32_t ay = hy[0] + 4 * hy[1] + 6 * hy[2] + 4 * hy[3] + hy[4] + 0x00800080u;
+            return fix(__builtin_amdgcn_perm(ay, ax, 0x07050301u));
+        };
+        // one level row on its own (the halo rows): five source rows, loads issued together
+        auto direct = [&](int y) {
+            uint32_t d[5][2], hx[5], hy[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ld_src(2 * y - 2 + k, d[k][0], d[k][1]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) hsum(d[k][0], d[k][1], hx[k], hy[k]);
+            return vert(hx, hy);
+        };
+        uint32_t hx[5], hy[5];
+        {
+            uint32_t d[5][2];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ld_src(2 * y0 - 2 + k, d[k][0], d[k][1]);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) hsum(d[k][0], d[k][1], hx[k], hy[k]);
+        }
+        uint32_t p0, p1, q0, q1;                           // source rows 2y+3, 2y+4, in flight
+        ld_src(2 * y0 + 3, p0, p1);
+        ld_src(2 * y0 + 4, q0, q1);
+        uint32_t vu = direct(refl101(y0 - 1, ho));
+        uint32_t vc = vert(hx, hy);
+        put_row(y0, vc);
+        for (int y = y0; y < y1; ++y) {
+            uint32_t vl;
+            if (y + 1 < y1) {
+                hx[0] = hx[2]; hy[0] = hy[2];
+                hx[1] = hx[3]; hy[1] = hy[3];
+                hx[2] = hx[4]; hy[2] = hy[4];
+                hsum(p0, p1, hx[3], hy[3]);
+                hsum(q0, q1, hx[4], hy[4]);
+                ld_src(2 * y + 5, p0, p1);
+                ld_src(2 * y + 6, q0, q1);
+                vl = vert(hx, hy);
+                put_row(y + 1, vl);
+            } else {
+                vl = direct(refl101(y1, ho));
+            }
+            put_der(y, vu, vc, vl);
+            vu = vc;
+            vc = vl;
+        }
+    }
+}
+
 // Scharr (calcSharrDeriv) of one level: interleaved int16 (dx, dy) pairs, zero outside the
 // image (the derivative image's constant border); 4 pixels (16 bytes) per lane
 __global__ void __launch_bounds__(256) k_scharr(const uint8_t* __restrict__ pyr, int64_t pstride,
@@ -1998,6 +2204,8 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
         dim3 g(tx0 > tx1 ? tx0 : tx1, ty0 + ty1, d->B);
         hipLaunchKernelGGL(k_pyr01, g, dim3(256), 0, VO_STREAM(stream), A0, A1, tx0, ty0, tx1);
     }
+    // row-streaming single-wave levels (k_pyr_rows) unless VO_PYR_ROWS=0 (the tile kernels)
+    static const int rows_env = [] { const char* e = getenv("VO_PYR_ROWS"); return e ? atoi(e) : 1; }();
     for (int l = fuse01 ? 2 : 0; l < d->nlev; ++l) {
         PyrLevelArgs A;
         if (l == 0) {
@@ -2012,6 +2220,16 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
         A.level = l;
         const int pw = A.w + 2 * VO_BORDER, ph = A.h + 2 * VO_BORDER;
         if (A.pitch % 64 || A.pitch < pw) return VO_EARG;
+        if (rows_env != 0) {
+            // rows per wave: 16, fewer on small levels so that a launch still has >= 8k waves
+            const int ns = ((pw + 3) / 4 * 4 + PR_STEP - 1) / PR_STEP;
+            int R = 16;
+            while (R > 4 && (int64_t)ns * ((A.h + R - 1) / R) * d->B < 8192) R >>= 1;
+            dim3 g(ns, (A.h + R - 1) / R, d->B);
+            if (l == 0) hipLaunchKernelGGL(k_pyr_rows<true>, g, dim3(64), 0, VO_STREAM(stream), A, R);
+            else hipLaunchKernelGGL(k_pyr_rows<false>, g, dim3(64), 0, VO_STREAM(stream), A, R);
+            continue;
+        }
         // level 0 (frame bytes, small LDS): 32-row tiles, half the blocks; pyrDown levels: 16
         if (l == 0) {
             dim3 g((pw + PT_W - 1) / PT_W, (ph + PYR0_TH - 1) / PYR0_TH, d->B);
