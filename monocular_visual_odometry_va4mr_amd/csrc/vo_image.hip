@@ -1096,29 +1096,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 // per sum (exact: |dI| <= 4080, weights <= 2^14)
                 const v2i16 wp0 = as_v2i16((uint32_t)(iw00 & 0xffff) | ((uint32_t)iw01 << 16));
                 const v2i16 wp1 = as_v2i16((uint32_t)(iw10 & 0xffff) | ((uint32_t)iw11 << 16));
-#ifdef VO_LK_TENSOR_BATCH
-                // diagnostics build (the round-4 variant that was dropped): the
-                // level's 24 tensor LDS reads issued together ahead of a scheduling barrier
-                uint32_t tdq[MAXJ][4];
-                int tsv[MAXJ][4];
-#pragma unroll
-                for (int j = 0; j < MAXJ; ++j) {
-                    const uint8_t* s = ir8 + toff[j] + ish;
-                    const uint32_t* d = DR + toff[j];
-                    tdq[j][0] = d[0]; tdq[j][1] = d[1]; tdq[j][2] = d[QS]; tdq[j][3] = d[QS + 1];
-                    tsv[j][0] = s[0]; tsv[j][1] = s[1]; tsv[j][2] = s[QS]; tsv[j][3] = s[QS + 1];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
                 for (int j = 0; j < MAXJ; ++j) {
 #ifdef VO_LKX_NOTENSOR
                     const uint32_t d00 = (uint32_t)(toff[j] * 977) & 0x03ff03ffu, d01 = d00 + 3, d10 = d00 + 5, d11 = d00 + 9;
                     const int v = (toff[j] * 31) & 8191;
-#elif defined(VO_LK_TENSOR_BATCH)
-                    const uint32_t d00 = tdq[j][0], d01 = tdq[j][1], d10 = tdq[j][2], d11 = tdq[j][3];
-                    const int v = DESCALE(__mul24(tsv[j][0], iw00) + __mul24(tsv[j][1], iw01) +
-                                          __mul24(tsv[j][2], iw10) + __mul24(tsv[j][3], iw11), 9);
 #else
                     const uint8_t* s = ir8 + toff[j] + ish;
                     const uint32_t* d = DR + toff[j];
