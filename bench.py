@@ -52,7 +52,7 @@ from monocular_visual_odometry_va4mr_amd.synth import Renderer, poses  # noqa: E
 from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E402
 
 SEQ_LEN = 4541          # KITTI seq00 frame count
-SEQ_OVERLAP = 30        # frames shared by neighbouring shards of the sequence job (--seq-overlap)
+SEQ_OVERLAP = 15        # frames shared by neighbouring shards of the sequence job (--seq-overlap)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s
 MFMA_PEAK_TF = 2500.0   # dense bf16 MFMA (no sparsity)
 MFMA_PEAK_I8 = 5000.0   # dense int8 MFMA: 32x32x32 in the cycles of bf16 32x32x16 (MI355X_MICROARCH.md)
@@ -296,16 +296,16 @@ def c5_leg(device, chains=256, steps=6, warmup=2, groups=2):
 
 def seq_chains_for(world: int) -> int:
     """Shards per GPU of the whole-sequence job.  The wall time is bootstrap(B) + (SEQ_LEN /
-    (world B) + 27) x step(B).  Measured on one GPU with two stream groups
-    (profiles/r4_seq_prio0_sweep.jsonl, r4_seq_small_sweep.jsonl): B = 64 gives 0.031 s +
-    98 x 1.24 ms, B = 32 0.018 s + 98 x 0.80 ms, B = 16 (one group) 0.013 s + 98 x 0.75 ms.  So
-    64 on one GPU, and 32 per GPU beyond (64, 128, 256 shards on 2, 4, 8 GPUs: ~0.097, 0.069,
-    0.054 s by the model, against 0.087 s and 0.060 s for 16 per GPU on 4 and 8).  Reference
-    fixtures exist for every resulting cut."""
-    return 64 if world <= 1 else 32
+    (world B) + overlap - 3) x step(B).  Measured at the 15-frame overlap with
+    the row-streaming pyramid, rank 0's slice of each plan run alone on one GPU (median of 3-5
+    runs, profiles/r5l_slice_sweep_o15*.jsonl): one GPU 48 -> 0.125 s, 64 -> 0.126 s; two GPUs
+    48 -> 0.082 s (64: 0.087, 32: 0.108); four 48 -> 0.060 s (64: 0.067, 32: 0.072); eight 24 ->
+    0.041-0.056 s (32: 0.043-0.057, 16: 0.065).  So 48 per GPU up to four GPUs and 24 beyond
+    (48, 96, 192, 192 shards on 1, 2, 4, 8 GPUs); reference fixtures hold every one of these cuts."""
+    return 48 if world <= 4 else 24
 
 
-def sequence_leg(device, seed, rank, world, per_gpu=64, groups=None, reps=3, overlap=SEQ_OVERLAP):
+def sequence_leg(device, seed, rank, world, per_gpu=48, groups=None, reps=3, overlap=SEQ_OVERLAP):
     """The whole C2 sequence as one job: SEQ_LEN frames cut into
     world x per_gpu overlapping shards (`overlap` frames shared), per_gpu chains on every rank (the
     shards per GPU are the batch dimension, main.py:166-175's loop split across chains),

@@ -1,7 +1,7 @@
 """Sharded run of one sequence across chains and GPUs, end to end.
 
     python -m monocular_visual_odometry_va4mr_amd.run_sequence --preset kitti --frames 4541 \
-        --shards-per-gpu 8 [--overlap 30] [--out poses.txt]
+        --shards-per-gpu 8 [--overlap 15] [--out poses.txt]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         -m monocular_visual_odometry_va4mr_amd.run_sequence ...
 
@@ -317,7 +317,7 @@ def main():
     ap.add_argument("--preset", default="kitti")
     ap.add_argument("--frames", type=int, default=600)
     ap.add_argument("--shards-per-gpu", type=int, default=8)
-    ap.add_argument("--overlap", type=int, default=30)
+    ap.add_argument("--overlap", type=int, default=15)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--reference", default=None, help="per-shard reference trajectories (.npz)")
     ap.add_argument("--out", default=None, help="write the stitched positions (frame segment x y z)")

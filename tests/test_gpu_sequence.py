@@ -95,7 +95,8 @@ def _shard_fixture(n_shards, overlap=30):
 
 
 @pytest.mark.parametrize("n_shards,groups,overlap", [(16, 1, 30), (8, 1, 30), (32, 2, 30), (64, 1, 30), (64, 2, 30),
-                                                     (128, 2, 30), (256, 2, 30), (64, 2, 15), (256, 2, 15)])
+                                                     (128, 2, 30), (256, 2, 30), (48, 2, 15), (64, 2, 15), (96, 2, 15),
+                                                     (192, 2, 15), (256, 2, 15)])
 def test_sharded_sequence_matches_reference_per_shard(n_shards, groups, overlap):
     from monocular_visual_odometry_va4mr_amd.run_sequence import reference_shards, run
     path, g = _shard_fixture(n_shards, overlap)
