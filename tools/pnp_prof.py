@@ -8,7 +8,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["VO_HIP_LIB"] = os.path.join(HERE, "monocular_visual_odometry_va4mr_amd", "_build", "libvo_hip_pnpprof.so")
+os.environ.setdefault("VO_HIP_LIB", os.path.join(HERE, "monocular_visual_odometry_va4mr_amd", "_build", "libvo_hip_pnpprof.so"))
 sys.path.insert(0, HERE)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
