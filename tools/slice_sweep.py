@@ -6,7 +6,7 @@ process group).  Prints one JSON line per configuration: the median wall of --re
 runs listed), bootstrap, steps, ms per step, the predicted job rate 4541 / wall, and the
 per-shard comparison with the reference class's runs when a fixture holds that cut.
 
-    python tools/slice_sweep.py W:B:O [W:B:O ...] [--reps 3]
+    python tools/slice_sweep.py W:B:O[:G] [W:B:O[:G] ...] [--reps 3]
 """
 import json
 import os
@@ -28,12 +28,14 @@ def main():
         argv = argv[:i] + argv[i + 2:]
     dev = torch.device("cuda", 0)
     for spec in argv:
-        world, B, O = (int(v) for v in spec.split(":"))
+        parts = [int(v) for v in spec.split(":")]
+        world, B, O = parts[:3]
+        G = parts[3] if len(parts) > 3 else None         # stream groups (default: run_sequence's)
         ref = reference_for(os.path.join(ROOT, "tests", "golden"), world * B, O)
         runs = []
         for _ in range(reps):
             runs.append(run("kitti", 4541, B, overlap=O, seed=1, device=dev, rank=0, world=world, reference=ref,
-                            time_boot=False))
+                            time_boot=False, groups=G))
             torch.cuda.empty_cache()
         r = sorted(runs, key=lambda x: x["wall_s"])[len(runs) // 2]
         vs = r.get("vs_reference") or {}
