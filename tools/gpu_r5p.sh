@@ -3,9 +3,9 @@
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
 BASE=$PWD/monocular_visual_odometry_va4mr_amd/_build/libvo_base.so
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bootstrap.py tests/test_gpu_configs.py -k "sift or bootstrap or c5" > gpurun_out/r5p_tests.log 2>&1 || { tail -30 gpurun_out/r5p_tests.log; exit 1; }
-tail -1 gpurun_out/r5p_tests.log
-out=gpurun_out/r5p_ab.jsonl; : > $out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bootstrap.py tests/test_gpu_configs.py -k "sift or bootstrap or c5" > gpurun_out/${TAG:-r5p}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG:-r5p}_tests.log; exit 1; }
+tail -1 gpurun_out/${TAG:-r5p}_tests.log
+out=gpurun_out/${TAG:-r5p}_ab.jsonl; : > $out
 sb() { local tag=$1; shift; env "$@" timeout -k 10 200 python -u tools/sift_bench.py 3 kitti 2> gpurun_out/sb.err | python3 -c "
 import json,sys
 for l in sys.stdin: d=json.loads(l); d['tag']='$tag'; print(json.dumps(d))" | tee -a $out; }
