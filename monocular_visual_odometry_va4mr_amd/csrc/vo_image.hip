@@ -1495,6 +1495,9 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
     int hsA = 0, hdA = 0, hsB = 0, hdB = 0;              // Sobel row terms of image rows ir-2, ir-1
     int xA = 0, yA = 0, zA = 0, xB = 0, yB = 0, zB = 0;  // box row sums (xx, xy, yy) of rows pr-2, pr-1
     float eA = 0.f, eB = 0.f;                            // eigen rows r-2, r-1
+    // the NMS maxima of those rows, each formed once when its row is new: 3-neighbour max of
+    // row r-2, left / right max of row r-1 (fmaxf is exact and order-free on these values)
+    float mA3 = 0.f, mB2 = 0.f;
     // eigen row r from the box row sums of rows r-1, r, r+1; then the NMS of row r-1
     auto eig_row = [&](int r, int ax, int ay, int az, int bx, int by, int bz, int cx, int cy, int cz) {
         const int sxx = ax + bx + cx, sxy = ay + by + cy, syy = az + bz + cz;
@@ -1507,12 +1510,11 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
             if (P.eig_out) P.eig_out[(int64_t)b * W * H + (int64_t)r * W + c] = v;
         }
         const int rn = r - 1;
+        const int iV = __float_as_int(v);
+        const float mV2 = fmaxf(__int_as_float(dpp_from_left(iV)), __int_as_float(dpp_from_right(iV)));
         if (rn >= o0 && rn < o1) {
-            const int iA = __float_as_int(eA), iB = __float_as_int(eB), iV = __float_as_int(v);
-            const float mA = fmaxf(fmaxf(__int_as_float(dpp_from_left(iA)), eA), __int_as_float(dpp_from_right(iA)));
-            const float mV = fmaxf(fmaxf(__int_as_float(dpp_from_left(iV)), v), __int_as_float(dpp_from_right(iV)));
-            const float mB = fmaxf(__int_as_float(dpp_from_left(iB)), __int_as_float(dpp_from_right(iB)));
-            const bool cand = nms_col && out && eB > 0.f && eB >= fmaxf(fmaxf(mA, mV), mB);
+            const float mV = fmaxf(mV2, v);
+            const bool cand = nms_col && out && eB > 0.f && eB >= fmaxf(fmaxf(mA3, mV), mB2);
             const uint64_t m = __ballot(cand);
             if (m) {
                 if (cand) {
@@ -1523,6 +1525,8 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
                 if (nbuf > E3_CAP - 64) flush();
             }
         }
+        mA3 = fmaxf(mB2, eB);
+        mB2 = mV2;
         eA = eB;
         eB = v;
     };
@@ -1533,11 +1537,15 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
     const int ir_end = g1 + 1;
 #pragma unroll
     for (int k = 0; k < E3_PF; ++k) pf[k] = (g0 - 1 + k <= ir_end) ? colp[(int64_t)(g0 - 1 + k) * P.pitch] : 0;
-    for (int ir = g0 - 1; ir <= ir_end; ++ir) {
-        const int iv = pf[0];
+    // rows in groups of E3_PF, unrolled: ring slot u holds row ir0 + u, and the row registers
+    // (A / B rings) are renamed instead of moved every row
+    for (int ir0 = g0 - 1; ir0 <= ir_end; ir0 += E3_PF) {
 #pragma unroll
-        for (int k = 0; k < E3_PF - 1; ++k) pf[k] = pf[k + 1];
-        pf[E3_PF - 1] = (ir + E3_PF <= ir_end) ? colp[(int64_t)(ir + E3_PF) * P.pitch] : 0;
+    for (int u = 0; u < E3_PF; ++u) {
+        const int ir = ir0 + u;
+        if (ir > ir_end) break;
+        const int iv = pf[u];
+        pf[u] = (ir + E3_PF <= ir_end) ? colp[(int64_t)(ir + E3_PF) * P.pitch] : 0;
         const int il = dpp_from_left(iv), irt = dpp_from_right(iv);
         const int hs = il + 2 * iv + irt, hd = irt - il;
         if (ir >= g0 + 1) {
@@ -1565,6 +1573,7 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
         }
         hsA = hsB; hdA = hdB;
         hsB = hs; hdB = hd;
+    }
     }
     if (out && nbuf) flush();
 #pragma unroll
