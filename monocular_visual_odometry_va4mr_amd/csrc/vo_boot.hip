@@ -510,6 +510,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
         return;
     }
     uint64_t rng = ~0ULL;
+    double lnum = 0.0;      // thread 0: log(1 - prob), formed at the first improvement
+    bool have_lnum = false;
     if (tid == 0) { sh[0] = 0; sh[1] = A.max_iters > 1 ? A.max_iters : 1; sh[2] = 0; }
     __syncthreads();
     // one block per CU (WPE 1): each hypothesis on 10 lanes (five_point_grp), 6 per wave, 24 per
@@ -587,7 +589,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8
                             if (good > (best > 4 ? best : 4)) {
                                 best = good;
                                 for (int q = 0; q < 9; ++q) bestE[q] = models[90 * hh + 9 * m + q];
-                                niters = ransac_update_niters(A.prob, (double)(n - good) / n, 5, niters);
+                                if (!have_lnum) { lnum = ransac_log_num(A.prob); have_lnum = true; }
+                                niters = ransac_update_niters_ln(lnum, (double)(n - good) / n, 5, niters);
                             }
                         }
                     }

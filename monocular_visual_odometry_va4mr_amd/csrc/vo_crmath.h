@@ -429,8 +429,17 @@ VO_CR double vcr_log(double x)
     const vcr_dd num = vcr_mk(m - 1.0, 0.0);               /* exact (Sterbenz) */
     const vcr_dd u = vcr_div(num, vcr_two_sum(m, 1.0));
     const vcr_dd u2 = vcr_mul(u, u);
+    /* terms 1..n with u^(2(n+1)) < 7.7e-34 (the tail is below 2^-110 of p; at most 22, the
+       count |u| < 0.172 needs): near x = 1, the RANSAC update's usual input, a third of them */
+    int n = 1;
+    double t = u2.hi;
+    while (n < 22) {
+        t *= u2.hi;
+        if (t < 7.7e-34) break;
+        ++n;
+    }
     vcr_dd p = vcr_mk(1.0, 0.0);                           /* 1 + u^2/3 + u^4/5 + ... */
-    for (int k = 22; k >= 1; --k)                          /* p = 1 + u^2 p (2k-1) / (2k+1) */
+    for (int k = n; k >= 1; --k)                           /* p = 1 + u^2 p (2k-1) / (2k+1) */
         p = vcr_add_d(vcr_mul(vcr_mul(u2, p), vcr_tab(VCR_LOG_C, k)), 1.0);
     vcr_dd r = vcr_mul_d(vcr_mul(u, p), 2.0);
     r = vcr_add(r, vcr_mul_d(vcr_mk(VCR_LN2_HI, VCR_LN2_LO), (double)e));

@@ -23,7 +23,7 @@ VO_DEV void svd_jacobi(double* A, double* w, double* V)
 #pragma unroll
         for (int j = 0; j < N; ++j) V[i * N + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 60; ++sweep) {
-        int changed = 0;
+        bool changed = false;
 #pragma unroll
         for (int i = 0; i < N - 1; ++i) {
 #pragma unroll
@@ -38,7 +38,7 @@ VO_DEV void svd_jacobi(double* A, double* w, double* V)
                 }
                 if (alpha == 0.0 || beta == 0.0) continue;
                 if (fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta)) continue;
-                changed = 1;
+                changed = true;
                 double zeta = (beta - alpha) / (2.0 * gamma);
                 double t = 1.0 / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                 if (zeta < 0) t = -t;
@@ -248,8 +248,11 @@ VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
                 pg += ai * aj;
             }
             const double alpha = quad_sum_f64(pa), beta = quad_sum_f64(pb), gamma = quad_sum_f64(pg);
-            if (alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta))) {
-                changed = true;
+            // skip test and rotation side by side, the rotation kept by selects (no branch:
+            // the test's sqrt overlaps the rotation's division chain)
+            const bool rot = alpha != 0.0 && beta != 0.0 && !(fabs(gamma) <= DBL_EPSILON * sqrt(alpha * beta));
+            changed |= rot;
+            {
                 const double zeta = (beta - alpha) / (2.0 * gamma);
                 const double u = fabs(zeta) + sqrt(1.0 + zeta * zeta);
                 const double wn = sqrt(u * u + 1.0);
@@ -258,12 +261,14 @@ VO_DEV void svd_jacobi_wave_rr(double* A, double* w, double* V, double* cs)
 #pragma unroll
                 for (int k = 0; k < MQ; ++k) {
                     const double xi = lo ? x[k] : px[k], xj = lo ? px[k] : x[k];
-                    x[k] = lo ? c * xi - s * xj : s * xi + c * xj;
+                    const double xr = lo ? c * xi - s * xj : s * xi + c * xj;
+                    x[k] = rot ? xr : x[k];
                 }
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) {
                     const double vi = lo ? v[k] : pv[k], vj = lo ? pv[k] : v[k];
-                    v[k] = lo ? c * vi - s * vj : s * vi + c * vj;
+                    const double vr = lo ? c * vi - s * vj : s * vi + c * vj;
+                    v[k] = rot ? vr : v[k];
                 }
             }
         }
@@ -807,16 +812,25 @@ VO_DEV float pnp_err(const double* R, const double* t, const CamK& k, float X0, 
     return du * du + dv * dv;
 }
 
-VO_DEV int ransac_update_niters(double p, double ep, int model_points, int max_iters)
+// RANSACUpdateNumIters split in two: the numerator log(max(1 - p, DBL_MIN)) depends only on the
+// confidence, so a RANSAC loop forms it once and passes it to every update (same values as
+// forming it per call; the early `denom < DBL_MIN` return does not depend on it)
+VO_DEV double ransac_log_num(double p)
 {
     p = p < 0 ? 0 : (p > 1 ? 1 : p);
+    return vcr_log(1. - p > DBL_MIN ? 1. - p : DBL_MIN);
+}
+VO_DEV int ransac_update_niters_ln(double lnum, double ep, int model_points, int max_iters)
+{
     ep = ep < 0 ? 0 : (ep > 1 ? 1 : ep);
-    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
     double denom = 1. - vcr_powi(1. - ep, model_points);
     if (denom < DBL_MIN) return 0;
-    num = vcr_log(num);
     denom = vcr_log(denom);
-    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+    return (denom >= 0 || -lnum >= max_iters * (-denom)) ? max_iters : (int)rint(lnum / denom);
+}
+VO_DEV int ransac_update_niters(double p, double ep, int model_points, int max_iters)
+{
+    return ransac_update_niters_ln(ransac_log_num(p), ep, model_points, max_iters);
 }
 
 VO_DEV float sampson_err(const double* E, double x1, double y1, double x2, double y2)

@@ -24,7 +24,9 @@ extern "C" int vo_pnp_prof_read(long long* out)
 namespace {
 #define PNPPROF(i) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pnpprof[i] = wall_clock64(); } while (0)
 #define PNPVAL(i, v) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_pnpprof[i] = (v); } while (0)
+#define PNPPROF_T(i, t) do { if (threadIdx.x == (t) && blockIdx.x == 0) g_pnpprof[i] = wall_clock64(); } while (0)
 #else
+#define PNPPROF_T(i, t) do { } while (0)
 #define PNPPROF(i) do { } while (0)
 #define PNPVAL(i, v) do { } while (0)
 #endif
@@ -333,6 +335,7 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         default: epnp_mtm_part<60, 78>(n, alphas, us, fu, fv, uc, vc, up); break;
     }
     __syncthreads();
+    PNPPROF(16);
     // 12x12 round-robin Jacobi SVD of M^T M by wave 0 in LDS (oracle: svd_jacobi_rr)
     if (wave_id() == 0) {
         for (int q = lane_id(); q < 144; q += 64) {
@@ -354,50 +357,56 @@ VO_DEV void epnp_block(EpnpShared& S, const double* K, const double* pws, const 
         }
     }
     __syncthreads();
-    // the three beta approximations are independent: one thread each, on different waves
-    if (tid == 0) {
-        {
-            double A[24], b4[4];
-            const int cols[4] = {0, 1, 3, 6};
-            for (int i = 0; i < 6; ++i) for (int j = 0; j < 4; ++j) A[i * 4 + j] = S.L[i * 10 + cols[j]];
-            lsq_svd<6, 4>(A, S.rho, b4);
-            double* B = S.betas[1];
-            if (b4[0] < 0) { B[0] = sqrt(-b4[0]); B[1] = -b4[1] / B[0]; B[2] = -b4[2] / B[0]; B[3] = -b4[3] / B[0]; }
-            else { B[0] = sqrt(b4[0]); B[1] = b4[1] / B[0]; B[2] = b4[2] / B[0]; B[3] = b4[3] / B[0]; }
-            epnp_gauss_newton(S.L, S.rho, B);
-        }
-    } else if (tid == 64) {
-        {
-            double A[18], b3[3];
-            for (int i = 0; i < 6; ++i) for (int j = 0; j < 3; ++j) A[i * 3 + j] = S.L[i * 10 + j];
-            lsq_svd<6, 3>(A, S.rho, b3);
-            double* B = S.betas[2];
-            if (b3[0] < 0) { B[0] = sqrt(-b3[0]); B[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0; }
-            else { B[0] = sqrt(b3[0]); B[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0; }
-            if (b3[1] < 0) B[0] = -B[0];
-            B[2] = 0.0; B[3] = 0.0;
-            epnp_gauss_newton(S.L, S.rho, B);
-        }
-    } else if (tid == 128) {
-        {
-            double A[30], b5[5];
-            for (int i = 0; i < 6; ++i) for (int j = 0; j < 5; ++j) A[i * 5 + j] = S.L[i * 10 + j];
-            lsq_svd<6, 5>(A, S.rho, b5);
-            double* B = S.betas[3];
-            if (b5[0] < 0) { B[0] = sqrt(-b5[0]); B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0; }
-            else { B[0] = sqrt(b5[0]); B[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0; }
-            if (b5[1] < 0) B[0] = -B[0];
-            B[2] = b5[3] / B[0]; B[3] = 0.0;
-            epnp_gauss_newton(S.L, S.rho, B);
-        }
-    }
-    __syncthreads();
-    PNPPROF(12);
-    // the oracle runs approximation 1's R,t before computing approximation 2's betas; the
-    // betas do not depend on R,t, so computing all betas first is equivalent.  compute_R_and_t's
+    // the three beta approximations are independent: lane 0 of waves 0..2 computes one each,
+    // and its wave goes straight on to that approximation's compute_R_and_t (no block barrier
+    // between them, so the two shorter chains' R, t hide under the longest one's betas).  The
+    // oracle runs approximation 1's R,t before computing approximation 2's betas; the betas do
+    // not depend on R,t, so the order between approximations is immaterial.  compute_R_and_t's
     // world centroid pw0 is the same sum of the same points in the same order as the first
     // control point cws[0] (set with it above), so it is not summed again.
-    if (wave_id() < 3) epnp_R_and_t_wave(S, wave_id() + 1, K, pws, us, alphas, n);
+    const int wv = wave_id();
+    if (wv < 3) {
+        if (lane_id() == 0) {
+            if (wv == 0) {
+                double A[24], b4[4];
+                const int cols[4] = {0, 1, 3, 6};
+                for (int i = 0; i < 6; ++i) for (int j = 0; j < 4; ++j) A[i * 4 + j] = S.L[i * 10 + cols[j]];
+                lsq_svd<6, 4>(A, S.rho, b4);
+                PNPPROF_T(17, 0);
+                double* B = S.betas[1];
+                if (b4[0] < 0) { B[0] = sqrt(-b4[0]); B[1] = -b4[1] / B[0]; B[2] = -b4[2] / B[0]; B[3] = -b4[3] / B[0]; }
+                else { B[0] = sqrt(b4[0]); B[1] = b4[1] / B[0]; B[2] = b4[2] / B[0]; B[3] = b4[3] / B[0]; }
+                epnp_gauss_newton(S.L, S.rho, B);
+                PNPPROF_T(18, 0);
+            } else if (wv == 1) {
+                double A[18], b3[3];
+                for (int i = 0; i < 6; ++i) for (int j = 0; j < 3; ++j) A[i * 3 + j] = S.L[i * 10 + j];
+                lsq_svd<6, 3>(A, S.rho, b3);
+                PNPPROF_T(24, 64);
+                double* B = S.betas[2];
+                if (b3[0] < 0) { B[0] = sqrt(-b3[0]); B[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0; }
+                else { B[0] = sqrt(b3[0]); B[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0; }
+                if (b3[1] < 0) B[0] = -B[0];
+                B[2] = 0.0; B[3] = 0.0;
+                epnp_gauss_newton(S.L, S.rho, B);
+                PNPPROF_T(25, 64);
+            } else {
+                double A[30], b5[5];
+                for (int i = 0; i < 6; ++i) for (int j = 0; j < 5; ++j) A[i * 5 + j] = S.L[i * 10 + j];
+                lsq_svd<6, 5>(A, S.rho, b5);
+                PNPPROF_T(19, 128);
+                double* B = S.betas[3];
+                if (b5[0] < 0) { B[0] = sqrt(-b5[0]); B[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0; }
+                else { B[0] = sqrt(b5[0]); B[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0; }
+                if (b5[1] < 0) B[0] = -B[0];
+                B[2] = b5[3] / B[0]; B[3] = 0.0;
+                epnp_gauss_newton(S.L, S.rho, B);
+                PNPPROF_T(23, 128);
+            }
+        }
+        wave_lds_sync();
+        epnp_R_and_t_wave(S, wv + 1, K, pws, us, alphas, n);
+    }
     __syncthreads();
     PNPPROF(13);
     if (tid == 0) {
@@ -478,6 +487,8 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
     }
     PNPPROF(0);
     uint64_t rng = ~0ULL;   // only thread 0's copy is used
+    double lnum = 0.0;      // thread 0: log(1 - confidence), formed at the first improvement
+    bool have_lnum = false;
     if (tid == 0) { sh[0] = 0; sh[1] = A.iters > 1 ? A.iters : 1; sh[2] = 0; }
     __syncthreads();
     while (true) {
@@ -543,25 +554,38 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
             // scoring in the order the sequential rule below visits the hypotheses, one per wave
             // at a time: a hypothesis at or past the running adaptive iteration count is never
             // looked at, so the batches stop once it is reached (same result as scoring all CH)
-            const int w = wave_id(), lane = lane_id(), nw = blockDim.x >> 6;
-            for (int h0 = 0; h0 < CH; h0 += nw) {
-                if (it0 + h0 >= sh[1]) break;                         // block-uniform
-                const int h = h0 + w;
-                if (h < CH) {
-                    int c = 0;
-                    if (valid[h]) {
-                        const double* R = mdl[h];
-                        const double* t = mdl[h] + 9;
-                        for (int i = lane; i < n; i += 64)
-                            c += pnp_err(R, t, k, obj[3 * i], obj[3 * i + 1], obj[3 * i + 2], img[2 * i], img[2 * i + 1]) <= A.thr;
-                        c = wave_sum_i32(c);
+            // Two hypotheses per wave per batch (h and h + nw), scored in one pass over the points
+            // (each point loaded once, two independent error chains): with the usual adaptive
+            // counts (2-8) the first batch already reaches the final count.
+            const int w = wave_id(), lane = lane_id(), nw = blockDim.x >> 6, HB = 2 * nw;
+            for (int h0 = 0; h0 < CH; h0 += HB) {
+                const int nit = sh[1];
+                if (it0 + h0 >= nit) break;                           // block-uniform
+                const int ha = h0 + w, hb = h0 + w + nw;
+                // a hypothesis at or past the running count is never looked at by the rule below
+                const bool va = ha < CH && it0 + ha < nit && valid[ha];
+                const bool vb = hb < CH && it0 + hb < nit && valid[hb];
+                if (va || vb) {
+                    const double* Ra = mdl[va ? ha : hb];
+                    const double* Rb = mdl[vb ? hb : ha];
+                    int ca = 0, cb = 0;
+                    for (int i = lane; i < n; i += 64) {
+                        const float X0 = obj[3 * i], X1 = obj[3 * i + 1], X2 = obj[3 * i + 2], u = img[2 * i], v = img[2 * i + 1];
+                        if (va) ca += pnp_err(Ra, Ra + 9, k, X0, X1, X2, u, v) <= A.thr;
+                        if (vb) cb += pnp_err(Rb, Rb + 9, k, X0, X1, X2, u, v) <= A.thr;
                     }
-                    if (lane == 0) cnt[h] = c;
+                    if (va) ca = wave_sum_i32(ca);
+                    if (vb) cb = wave_sum_i32(cb);
+                    if (lane == 0) {
+                        if (va) cnt[ha] = ca;
+                        if (vb) cnt[hb] = cb;
+                    }
                 }
                 __syncthreads();
+                if (h0 == 0) PNPPROF(28);
                 if (tid == 0) {
                     int niters = sh[1], best = sh[2];
-                    const int h1 = h0 + nw < CH ? h0 + nw : CH;
+                    const int h1 = h0 + HB < CH ? h0 + HB : CH;
                     for (int hh = h0; hh < h1; ++hh) {
                         if (it0 + hh >= niters) break;
                         if (!valid[hh]) continue;
@@ -569,13 +593,15 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
                         if (good > (best > 3 ? best : 3)) {
                             best = good;
                             for (int q = 0; q < 12; ++q) bestm[q] = mdl[hh][q];
-                            niters = ransac_update_niters(A.conf, (double)(n - good) / n, 4, niters);
+                            if (!have_lnum) { lnum = ransac_log_num(A.conf); have_lnum = true; }
+                            niters = ransac_update_niters_ln(lnum, (double)(n - good) / n, 4, niters);
                         }
                     }
                     sh[1] = niters;
                     sh[2] = best;
                 }
                 __syncthreads();
+                if (h0 == 0) PNPPROF(29);
             }
         }
         if (tid == 0) sh[0] = it0 + CH;
@@ -961,8 +987,10 @@ VO_DEV void triangulate_block(const TriArgs& A)
     __shared__ TriShared sh;
     if (!tri_setup(A, sh)) return;
     tri_gate(A, sh);
+    PNPPROF(26);
     tri_solve(A, sh, sh.m, threadIdx.x, blockDim.x);
     __syncthreads();
+    PNPPROF(27);
     tri_append(A, sh);
 }
 

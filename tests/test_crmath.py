@@ -78,7 +78,11 @@ def test_exp2_log_powi_correctly_rounded(crm):
     rng = np.random.default_rng(2)
     y = np.concatenate([rng.uniform(-0.5, 2.5, 1500), [0.0, 1.0, 1 / 3, 2 / 3]])
     assert np.array_equal(crm(3, y), _rn(lambda v: mpmath.power(2, v), y))
-    x = np.concatenate([rng.uniform(1e-12, 1, 1500), rng.uniform(0.9, 1.1, 500), [0.01, 1.0, 2.0, 1e-300]])
+    # the series length adapts to |u| = |m - 1| / (m + 1): inputs near 1 (few terms) and near
+    # sqrt(1/2) 2^k (the full 22) are both covered
+    x = np.concatenate([rng.uniform(1e-12, 1, 1500), rng.uniform(0.9, 1.1, 500), 1 - rng.uniform(0, 1e-6, 300),
+                        np.sqrt(0.5) * 2.0 ** rng.integers(-20, 20, 200) * (1 + rng.uniform(-1e-3, 1e-3, 200)),
+                        [0.01, 1.0, 2.0, 1e-300]])
     assert np.array_equal(crm(4, x), _rn(mpmath.log, x))
     for n in (4, 5):
         b = rng.uniform(0, 1, 800)

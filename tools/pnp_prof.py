@@ -31,8 +31,10 @@ eng.bootstrap(fr[0:1], fr[1:2])
 lib = L.lib()
 lib.vo_pnp_prof_read.argtypes = [C.c_void_p]
 buf = (C.c_longlong * 32)()
-names = [("ransac", 0, 3), ("r:prior rounds", 0, 1), ("r:subsets", 1, 6), ("r:p3p", 6, 2), ("r:score", 2, 3), ("inl+compact", 3, 4), ("epnp prep", 4, 10), ("MtM+svd", 10, 11), ("betas", 11, 12),
-         ("R,t x3", 12, 13), ("pick", 13, 5), ("apply", 5, 14), ("triangulate", 14, 15), ("total", 0, 15)]
+names = [("ransac", 0, 3), ("r:prior rounds", 0, 1), ("r:subsets", 1, 6), ("r:p3p", 6, 2), ("r:score", 2, 3), ("s:score1", 2, 28), ("s:rule1", 28, 29), ("inl+compact", 3, 4), ("epnp prep", 4, 10), ("MtM", 10, 16), ("svd12", 16, 11), ("betas+Rt", 11, 13), ("b1:lsq", 11, 17), ("b1:gn", 17, 18),
+         ("b2:lsq", 11, 24), ("b2:gn", 24, 25), ("b3:lsq", 11, 19), ("b3:gn", 19, 23),
+         ("pick", 13, 5), ("apply", 5, 14), ("triangulate", 14, 15), ("t:gate", 14, 26), ("t:solve", 26, 27), ("t:append", 27, 15),
+         ("total", 0, 15)]
 acc = {k: [] for k, _, _ in names}
 for i in range(2, n):
     eng.step(fr[i:i + 1])
