@@ -820,13 +820,28 @@ VO_DEV double ransac_log_num(double p)
     p = p < 0 ? 0 : (p > 1 ? 1 : p);
     return vcr_log(1. - p > DBL_MIN ? 1. - p : DBL_MIN);
 }
-VO_DEV int ransac_update_niters_ln(double lnum, double ep, int model_points, int max_iters)
+// ... and the denominator part, which depends only on the inlier ratio: 0 when
+// 1 - (1 - ep)^mp < DBL_MIN (the update then returns 0), else 1 with *ld = log(1 - (1 - ep)^mp).
+// A RANSAC loop can form it for a batch of hypotheses in parallel and apply the sequential
+// rule with ransac_niters_fin afterwards (the same operations on the same values).
+VO_DEV int ransac_niters_den(double ep, int model_points, double* ld)
 {
     ep = ep < 0 ? 0 : (ep > 1 ? 1 : ep);
-    double denom = 1. - vcr_powi(1. - ep, model_points);
+    const double denom = 1. - vcr_powi(1. - ep, model_points);
     if (denom < DBL_MIN) return 0;
-    denom = vcr_log(denom);
-    return (denom >= 0 || -lnum >= max_iters * (-denom)) ? max_iters : (int)rint(lnum / denom);
+    *ld = vcr_log(denom);
+    return 1;
+}
+VO_DEV int ransac_niters_fin(double lnum, int ok, double ld, int max_iters)
+{
+    if (!ok) return 0;
+    return (ld >= 0 || -lnum >= max_iters * (-ld)) ? max_iters : (int)rint(lnum / ld);
+}
+VO_DEV int ransac_update_niters_ln(double lnum, double ep, int model_points, int max_iters)
+{
+    double ld = 0.0;
+    const int ok = ransac_niters_den(ep, model_points, &ld);
+    return ransac_niters_fin(lnum, ok, ld, max_iters);
 }
 VO_DEV int ransac_update_niters(double p, double ep, int model_points, int max_iters)
 {

@@ -448,7 +448,69 @@ struct PnPArgs {
     int32_t* n_inl;         // [B]
 };
 
-VO_DEV void pnp_ransac_block(const PnPArgs& A)
+// getSubset for CH hypotheses (oracle get_subset: four draws rng % n per hypothesis, a draw equal
+// to an earlier one of the same hypothesis drawn again), by one whole wave.  Lane 0 runs the
+// generator -- one multiply-add per value, no division -- for the 4 CH values a round without
+// repeats consumes, storing each value and the state after it; the lanes reduce them mod n in
+// parallel and check each hypothesis's four for a repeat.  The hypotheses before the first one
+// with a repeat take their four values as drawn; from that one on, lane 0 applies the serial rule
+// to the stored values (drawing past them if it needs more): the same draws in the same order.
+// rng (lane 0's copy) ends past the last value used.
+VO_DEV void pnp_subsets(int CH, uint32_t un, uint64_t& rng, int (*sub)[4], uint32_t* res, uint64_t* st)
+{
+    const int lane = lane_id(), R = 4 * CH;
+    if (lane == 0) {
+        uint64_t g = rng;
+        for (int i = 0; i < R; ++i) {
+            g = (uint64_t)(uint32_t)g * 4164903690ULL + (g >> 32);       // rng_next
+            res[i] = (uint32_t)g;
+            st[i] = g;
+        }
+    }
+    wave_lds_sync();
+    for (int i = lane; i < R; i += 64) res[i] = res[i] % un;
+    wave_lds_sync();
+    int bad = CH;
+    for (int h0 = 0; h0 < CH; h0 += 64) {
+        const int h = h0 + lane;
+        bool rep = false;
+        if (h < CH) {
+            const uint32_t a = res[4 * h], b = res[4 * h + 1], c = res[4 * h + 2], d = res[4 * h + 3];
+            rep = b == a || c == a || c == b || d == a || d == b || d == c;
+        }
+        const unsigned long long m = __ballot(rep);
+        if (m) { bad = h0 + __ffsll((long long)m) - 1; break; }
+    }
+    for (int h = lane; h < bad; h += 64) {
+        sub[h][0] = (int)res[4 * h]; sub[h][1] = (int)res[4 * h + 1];
+        sub[h][2] = (int)res[4 * h + 2]; sub[h][3] = (int)res[4 * h + 3];
+    }
+    if (lane == 0) {
+        int p = 4 * bad;
+        uint64_t g = p > 0 ? st[p - 1] : rng;
+        auto draw = [&]() -> int {
+            int v;
+            if (p < R) { v = (int)res[p]; g = st[p]; }
+            else v = (int)(rng_next(g) % un);
+            ++p;
+            return v;
+        };
+        for (int h = bad; h < CH; ++h) {
+            const int s0 = draw();
+            int s1, s2, s3;
+            do { s1 = draw(); } while (s1 == s0);
+            do { s2 = draw(); } while (s2 == s0 || s2 == s1);
+            do { s3 = draw(); } while (s3 == s0 || s3 == s1 || s3 == s2);
+            sub[h][0] = s0; sub[h][1] = s1; sub[h][2] = s2; sub[h][3] = s3;
+        }
+        rng = g;
+    }
+}
+
+// defer (k_pnp_tri): on the refit path, leave the final pose in defer[0..12) (R row-major, t)
+// with *pend = 1 instead of forming rvec here, so that the epilogue's Rodrigues pair runs beside
+// its landmark compaction (pnp_apply_split); *pend stays as the caller set it (0) otherwise
+VO_DEV void pnp_ransac_block(const PnPArgs& A, double* defer = nullptr, int* pend = nullptr)
 {
     __shared__ int sub[HYP][4];
     __shared__ double mdl[HYP][12];
@@ -457,6 +519,11 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
     __shared__ int sh[8];
     __shared__ int lds16[16];
     __shared__ EpnpShared S;
+    __shared__ uint32_t sub_res[4 * HYP];
+    __shared__ uint64_t sub_st[4 * HYP];
+    __shared__ double den_ld[HYP];
+    __shared__ int den_ok[HYP];
+    __shared__ double lnum_sh;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     if (A.chain_status && A.chain_status[b] != 0) return;
@@ -487,8 +554,6 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
     }
     PNPPROF(0);
     uint64_t rng = ~0ULL;   // only thread 0's copy is used
-    double lnum = 0.0;      // thread 0: log(1 - confidence), formed at the first improvement
-    bool have_lnum = false;
     if (tid == 0) { sh[0] = 0; sh[1] = A.iters > 1 ? A.iters : 1; sh[2] = 0; }
     __syncthreads();
     while (true) {
@@ -499,19 +564,8 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
         // drops below it there, and fewer diverging P3P lanes and inlier counts finish sooner
         const int CH = it0 == 0 ? VO_PNP_CH1 : HYP;
         PNPPROF(1);
-        if (tid == 0) {
-            // getSubset (oracle get_subset): four distinct draws, kept in registers so the
-            // duplicate checks do not wait on LDS
-            const uint32_t un = (uint32_t)n;
-            for (int h = 0; h < CH; ++h) {
-                const int s0 = (int)(rng_next(rng) % un);
-                int s1, s2, s3;
-                do { s1 = (int)(rng_next(rng) % un); } while (s1 == s0);
-                do { s2 = (int)(rng_next(rng) % un); } while (s2 == s0 || s2 == s1);
-                do { s3 = (int)(rng_next(rng) % un); } while (s3 == s0 || s3 == s1 || s3 == s2);
-                sub[h][0] = s0; sub[h][1] = s1; sub[h][2] = s2; sub[h][3] = s3;
-            }
-        }
+        if (wave_id() == 0) pnp_subsets(CH, (uint32_t)n, rng, sub, sub_res, sub_st);
+        else if (it0 == 0 && tid == 64) lnum_sh = ransac_log_num(A.conf);    // log(1 - confidence), once
         __syncthreads();
         PNPPROF(6);
         {
@@ -583,22 +637,32 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
                 }
                 __syncthreads();
                 if (h0 == 0) PNPPROF(28);
-                if (tid == 0) {
-                    int niters = sh[1], best = sh[2];
+                if (w == 0) {
+                    // the expensive half of every update this batch can make (its log), one lane
+                    // per hypothesis; lane 0 then applies the sequential rule with them
                     const int h1 = h0 + HB < CH ? h0 + HB : CH;
-                    for (int hh = h0; hh < h1; ++hh) {
-                        if (it0 + hh >= niters) break;
-                        if (!valid[hh]) continue;
-                        const int good = cnt[hh];
-                        if (good > (best > 3 ? best : 3)) {
-                            best = good;
-                            for (int q = 0; q < 12; ++q) bestm[q] = mdl[hh][q];
-                            if (!have_lnum) { lnum = ransac_log_num(A.conf); have_lnum = true; }
-                            niters = ransac_update_niters_ln(lnum, (double)(n - good) / n, 4, niters);
-                        }
+                    const int hh = h0 + lane;
+                    if (hh < h1 && it0 + hh < nit && valid[hh]) {
+                        double ld = 0.0;
+                        den_ok[hh] = ransac_niters_den((double)(n - cnt[hh]) / n, 4, &ld);
+                        den_ld[hh] = ld;
                     }
-                    sh[1] = niters;
-                    sh[2] = best;
+                    wave_lds_sync();
+                    if (lane == 0) {
+                        int niters = sh[1], best = sh[2];
+                        for (int q = h0; q < h1; ++q) {
+                            if (it0 + q >= niters) break;
+                            if (!valid[q]) continue;
+                            const int good = cnt[q];
+                            if (good > (best > 3 ? best : 3)) {
+                                best = good;
+                                for (int r = 0; r < 12; ++r) bestm[r] = mdl[q][r];
+                                niters = ransac_niters_fin(lnum_sh, den_ok[q], den_ld[q], niters);
+                            }
+                        }
+                        sh[1] = niters;
+                        sh[2] = best;
+                    }
                 }
                 __syncthreads();
                 if (h0 == 0) PNPPROF(29);
@@ -646,7 +710,13 @@ VO_DEV void pnp_ransac_block(const PnPArgs& A)
     epnp_block(S, A.K, pws, us, alphas, pcs, m, Rfin, tfin);
     PNPPROF(5);
     if (tid == 0) {
-        rodrigues_m2v(Rfin, A.rvec + 3 * b);
+        if (defer) {
+            for (int q = 0; q < 9; ++q) defer[q] = Rfin[q];
+            for (int q = 0; q < 3; ++q) defer[9 + q] = tfin[q];
+            *pend = 1;
+        } else {
+            rodrigues_m2v(Rfin, A.rvec + 3 * b);
+        }
         for (int q = 0; q < 3; ++q) A.tvec[3 * b + q] = tfin[q];
         A.success[b] = 1;
         A.n_inl[b] = m;
@@ -710,6 +780,90 @@ VO_DEV void pnp_apply_block(const vo_dims& d, const vo_state& s, const double* r
         // multiply-adds -- reproduced here so the pose is bit-identical (tools/blas_order_probe.py)
         for (int i = 0; i < 3; ++i)
             tcw[i] = __builtin_fma(-Rcw[i * 3 + 2], t[2], __builtin_fma(-Rcw[i * 3 + 1], t[1], -Rcw[i * 3] * t[0]));
+    }
+}
+
+// pnp_apply_block for k_pnp_tri, after pnp_ransac_block(A, defer, pend): lane 0 of wave 0 forms
+// rvec from the deferred pose (Rodrigues, as pnp_ransac_block does), converts it back and writes
+// the inverted pose, while wave 1 compacts the landmarks on its own (a wave-level scan over four
+// 64-point chunks per pass, no block barrier): the same values in the same slots as
+// pnp_apply_block, the two serial parts side by side
+VO_DEV void pnp_apply_split(const vo_dims& d, const vo_state& s, double* rvec, const double* tvec,
+                            const int32_t* success, const uint8_t* mask_all, const double* defer, int pend)
+{
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    if (s.status[b] != 0) return;
+    const int n = s.nL[b];
+    if (n < 8) { if (tid == 0) s.status[b] = VO_ST_NOT_ENOUGH_KP; return; }
+    if (!success[b]) { if (tid == 0) s.status[b] = VO_ST_PNP_FAILED; return; }
+    if (w == 0) {
+        if (lane == 0) {
+            double rv[3], Rwc[9];
+            if (pend) {
+                rodrigues_m2v(defer, rv);
+                for (int q = 0; q < 3; ++q) rvec[3 * b + q] = rv[q];
+            } else {
+                for (int q = 0; q < 3; ++q) rv[q] = rvec[3 * b + q];
+            }
+            rodrigues_v2m(rv, Rwc);
+            const int f = s.nF[b];
+            if (f >= d.fcap) {
+                s.status[b] = VO_ST_CAPACITY;
+            } else {
+                double* Rcw = s.pose_R + ((int64_t)b * d.fcap + f) * 9;
+                double* tcw = s.pose_t + ((int64_t)b * d.fcap + f) * 3;
+                const double* t = tvec + 3 * b;
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) Rcw[i * 3 + j] = Rwc[j * 3 + i];
+                // invert_transform :74-75 in BLAS gemv's fused order (pnp_apply_block)
+                for (int i = 0; i < 3; ++i)
+                    tcw[i] = __builtin_fma(-Rcw[i * 3 + 2], t[2], __builtin_fma(-Rcw[i * 3 + 1], t[1], -Rcw[i * 3] * t[0]));
+            }
+        }
+    } else if (w == 1) {
+        const uint8_t* mask = mask_all + (int64_t)b * d.ncap;
+        float* X = s.lm_X + (int64_t)b * d.ncap * 3;
+        float* kp = s.lm_kp + (int64_t)b * d.ncap * 2;
+        const int kcap = d.ncap > d.pcap ? d.ncap : d.pcap;
+        float* outl = s.outl_kp + (int64_t)b * kcap * 2;
+        float* inl = s.inl_kp + (int64_t)b * kcap * 2;
+        const unsigned long long below = (1ull << lane) - 1ull;
+        int nin = 0, nout = 0;
+        for (int base = 0; base < n; base += 256) {
+            // loads of the four chunks first (every write of this pass lands below base + 256 and
+            // at or below its own source index, so no later read sees a moved point)
+            float x0[4], x1[4], x2[4], k0[4], k1[4];
+            bool in[4], valid[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = base + 64 * c + lane;
+                valid[c] = i < n;
+                in[c] = valid[c] && mask[i];
+                x0[c] = x1[c] = x2[c] = k0[c] = k1[c] = 0.f;
+                if (valid[c]) { x0[c] = X[3 * i]; x1[c] = X[3 * i + 1]; x2[c] = X[3 * i + 2]; k0[c] = kp[2 * i]; k1[c] = kp[2 * i + 1]; }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const unsigned long long mi = __ballot(in[c]), mv = __ballot(valid[c]);
+                const int pre = __popcll(mi & below), tin = __popcll(mi), tv = __popcll(mv);
+                const int pin = nin + pre, pout = nout + (lane - pre);      // valid lanes are a prefix
+                if (in[c]) {
+                    X[3 * pin] = x0[c]; X[3 * pin + 1] = x1[c]; X[3 * pin + 2] = x2[c];
+                    kp[2 * pin] = k0[c]; kp[2 * pin + 1] = k1[c];
+                    inl[2 * pin] = k0[c]; inl[2 * pin + 1] = k1[c];
+                } else if (valid[c]) {
+                    outl[2 * pout] = k0[c]; outl[2 * pout + 1] = k1[c];
+                }
+                nin += tin;
+                nout += tv - tin;
+            }
+        }
+        if (lane == 0) {
+            s.nL[b] = nin;
+            s.nInl[b] = nin;
+            s.nOutl[b] = nout;
+        }
     }
 }
 
@@ -1036,9 +1190,12 @@ k_pnp_tri(PnPArgs A, TriArgs T)
         track_compact_block(T.d, T.s);
         __syncthreads();
     }
-    pnp_ransac_block(A);
+    __shared__ double defer[12];
+    __shared__ int pend;
+    if (threadIdx.x == 0) pend = 0;
+    pnp_ransac_block(A, defer, &pend);
     __syncthreads();
-    pnp_apply_block(T.d, T.s, A.rvec, A.tvec, A.success, A.mask);
+    pnp_apply_split(T.d, T.s, A.rvec, A.tvec, A.success, A.mask, defer, pend);
     __syncthreads();
     PNPPROF(14);
     triangulate_block(T);
