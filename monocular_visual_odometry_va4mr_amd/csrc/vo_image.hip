@@ -290,25 +290,25 @@ __global__ void __launch_bounds__(256) k_pyr01(PyrLevelArgs A0, PyrLevelArgs A1,
 // row y reads rows y-1, y, y+1 (the chunk's two halo rows evaluated on their own, reflect-101
 // at the level's first and last row).  Same bytes and derivatives as pyr_tile.
 #define PR_STEP 248
+// one wave's item of a level: strip sx, rows sy R .. sy R + R - 1, chain b
 template <bool L0>
-__global__ void __launch_bounds__(64) k_pyr_rows(PyrLevelArgs A, int R)
+VO_DEV void pyr_rows_wave(const PyrLevelArgs& A, int R, int sx, int sy, int b)
 {
-    const int lane = threadIdx.x;
-    const int b = blockIdx.z;
+    const int lane = lane_id();
     const int wo = A.w, ho = A.h;
     const int pw = wo + 2 * VO_BORDER, ph = ho + 2 * VO_BORDER;
     const int pwa = (pw + 3) & ~3;
     const int ns = (pwa + PR_STEP - 1) / PR_STEP;
-    const bool lastst = (int)blockIdx.x == ns - 1;
-    const int base = lastst ? max(pwa - 252, -4) : (int)blockIdx.x * PR_STEP - 4;
+    const bool lastst = sx == ns - 1;
+    const int base = lastst ? max(pwa - 252, -4) : sx * PR_STEP - 4;
     const int px = base + 4 * lane;
-    const int y0 = (int)blockIdx.y * R;
-    if (y0 >= ho || (int)blockIdx.x >= ns) return;
+    const int y0 = sy * R;
+    if (y0 >= ho || sx >= ns) return;
     const int y1 = min(y0 + R, ho);
     // columns this wave writes: [lo, hi); the earlier strips stop short of the last one's range,
     // so a border column and the Scharr taps next to it come from one wave only
-    const int lo = lastst ? max(pwa - PR_STEP, 0) : (int)blockIdx.x * PR_STEP;
-    const int hi = lastst ? pwa : min((int)blockIdx.x * PR_STEP + PR_STEP, pwa - PR_STEP);
+    const int lo = lastst ? max(pwa - PR_STEP, 0) : sx * PR_STEP;
+    const int hi = lastst ? pwa : min(sx * PR_STEP + PR_STEP, pwa - PR_STEP);
     const bool wlane = lane >= 1 && lane <= 62 && px >= lo && px < hi && px < pw;
     const bool dlane = wlane && px + 3 >= VO_BORDER && px < VO_BORDER + wo;
     // per byte of the lane: the strip position (lane * 4 + byte) holding its value
@@ -475,6 +475,36 @@ __global__ void __launch_bounds__(64) k_pyr_rows(PyrLevelArgs A, int R)
             vu = vc;
             vc = vl;
         }
+    }
+}
+
+template <bool L0>
+__global__ void __launch_bounds__(64) k_pyr_rows(PyrLevelArgs A, int R)
+{
+    pyr_rows_wave<L0>(A, R, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
+}
+
+// The small pyrDown levels of few chains in one launch (round 5): one 16-wave block per chain
+// walks the levels in order, each wave taking (strip, row chunk) items of pyr_rows_wave, with a
+// block barrier between levels (a level reads the one before).  At a few chains each level
+// launch of k_pyr_rows was a ~12 us step of the frame's latency chain, mostly launch and
+// dependency wait; the same items give the same bytes.
+#define PYR_TAIL_MAX 6
+struct PyrTailArgs {
+    PyrLevelArgs a[PYR_TAIL_MAX];
+    int R[PYR_TAIL_MAX];
+    int n;
+};
+__global__ void __launch_bounds__(1024) k_pyr_tail(PyrTailArgs T)
+{
+    const int w = wave_id(), nw = (int)(blockDim.x >> 6);
+    for (int l = 0; l < T.n; ++l) {
+        const PyrLevelArgs& A = T.a[l];
+        const int R = T.R[l];
+        const int pwa = (A.w + 2 * VO_BORDER + 3) & ~3;
+        const int ns = (pwa + PR_STEP - 1) / PR_STEP, nch = (A.h + R - 1) / R;
+        for (int it = w; it < ns * nch; it += nw) pyr_rows_wave<false>(A, R, it % ns, it / ns, (int)blockIdx.x);
+        __syncthreads();
     }
 }
 
@@ -2197,7 +2227,37 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
     }
     // row-streaming single-wave levels (k_pyr_rows) unless VO_PYR_ROWS=0 (the tile kernels)
     static const int rows_env = [] { const char* e = getenv("VO_PYR_ROWS"); return e ? atoi(e) : 1; }();
-    for (int l = fuse01 ? 2 : 0; l < d->nlev; ++l) {
+    // levels 2.. of 9 to 64 chains in one launch (k_pyr_tail; VO_PYR_TAIL=0 / 1 forces it off /
+    // on).  Rank 0 of the 8-GPU sequence plan (2 groups of 12 chains) 79.5-80.9k -> 83.0-83.9k
+    // frames/s predicted; at one chain the per-level launches, with 48 waves a level instead of
+    // 16, are faster (2,250 vs 2,185 frames/s; profiles/r5_pyr_tail_ab.jsonl)
+    static const int tail_env = [] { const char* e = getenv("VO_PYR_TAIL"); return e ? atoi(e) : -1; }();
+    const int ltail = 2;
+    const bool tail = rows_env != 0 && d->nlev > ltail && d->nlev - ltail <= PYR_TAIL_MAX &&
+                      (tail_env >= 0 ? tail_env == 1 : d->B > 8 && d->B <= 64);
+    PyrTailArgs T;
+    T.n = 0;
+    if (tail) {
+        T.n = d->nlev - ltail;
+        for (int i = 0; i < T.n; ++i) {
+            const int l = ltail + i;
+            PyrLevelArgs& A = T.a[i];
+            A.src = s->pyr[cur]; A.sstride = d->pyr_stride;
+            A.sw = d->lvl_w[l - 1]; A.sh = d->lvl_h[l - 1]; A.spitch = d->lvl_pitch[l - 1]; A.soff = d->lvl_off[l - 1];
+            A.pyr = s->pyr[cur]; A.pstride = d->pyr_stride;
+            A.der = s->der[cur]; A.dstride = d->der_stride;
+            A.w = d->lvl_w[l]; A.h = d->lvl_h[l]; A.pitch = d->lvl_pitch[l]; A.off = d->lvl_off[l];
+            A.level = l;
+            if (A.pitch % 64 || A.pitch < A.w + 2 * VO_BORDER) return VO_EARG;
+            // about one item per wave of the 16-wave block
+            const int pwa = (A.w + 2 * VO_BORDER + 3) & ~3, ns = (pwa + PR_STEP - 1) / PR_STEP;
+            const int want = ns >= 16 ? 1 : 16 / ns;
+            int R = (A.h + want - 1) / want;
+            T.R[i] = R < 2 ? 2 : R;
+        }
+    }
+    const int lend = tail ? ltail : d->nlev;
+    for (int l = fuse01 ? 2 : 0; l < lend; ++l) {
         PyrLevelArgs A;
         if (l == 0) {
             A.src = frames; A.sstride = frame_stride; A.sw = A.sh = A.spitch = 0; A.soff = 0;
@@ -2235,6 +2295,7 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
             else hipLaunchKernelGGL((k_pyr_level<false, 16>), g, dim3(256), 0, VO_STREAM(stream), A);
         }
     }
+    if (tail) hipLaunchKernelGGL(k_pyr_tail, dim3(d->B), dim3(1024), 0, VO_STREAM(stream), T);
     return hip_ok() ? VO_OK : VO_EHIP;
 }
 

@@ -96,6 +96,36 @@ def test_pyramid_scharr_sizes(engine_factory, W, H):
             ref = O.pyrdown(ref)
 
 
+@pytest.mark.parametrize("W,H", [(1241, 376), (640, 480)])
+def test_pyramid_tail_many_chains(engine_factory, W, H):
+    """9 to 64 chains per launch take levels 2.. in one launch (k_pyr_tail, one 16-wave block per
+    chain): every chain's levels, derivatives and reflect-101 borders equal the oracle's."""
+    from oracle import _olib as O
+    from monocular_visual_odometry_va4mr_amd import _lib as L
+    B = 10
+    rng = np.random.default_rng(W + H)
+    imgs = rng.integers(0, 256, (B, H, W), dtype=np.uint8)
+    K = np.array([[300.0, 0, W / 2], [0, 300.0, H / 2], [0, 0, 1]])
+    eng, _ = engine_factory(K=K, B=B, W=W, H=H)
+    assert eng.dims.nlev >= 3
+    eng.build_pyramid(torch.from_numpy(imgs), 0)
+    torch.cuda.synchronize()
+    d = eng.dims
+    Bd = L.VO_BORDER
+    for b in range(B):
+        ref = imgs[b]
+        for lv in range(d.nlev):
+            w, h, p, o = d.lvl_w[lv], d.lvl_h[lv], d.lvl_pitch[lv], d.lvl_off[lv]
+            pp = eng.t["pyr0"][b, o:o + (h + 2 * Bd) * p].view(h + 2 * Bd, p).cpu().numpy()[:, :w + 2 * Bd]
+            ry = [O_refl(i - Bd, h) for i in range(h + 2 * Bd)]
+            rx = [O_refl(i - Bd, w) for i in range(w + 2 * Bd)]
+            assert np.array_equal(pp, ref[np.ix_(ry, rx)]), f"b={b} pyramid level {lv}"
+            n = (h + 2 * Bd) * p
+            full = eng.t["der0"][b].view(-1, 2)[o:o + n].view(h + 2 * Bd, p, 2).cpu().numpy()
+            assert np.array_equal(full[Bd:Bd + h, Bd:Bd + w], O.scharr(ref)), f"b={b} scharr level {lv}"
+            ref = O.pyrdown(ref)
+
+
 def O_refl(p, n):
     """cv::borderInterpolate(BORDER_REFLECT_101)"""
     if n == 1:
