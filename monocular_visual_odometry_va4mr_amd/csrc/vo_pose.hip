@@ -1329,6 +1329,128 @@ __global__ void __launch_bounds__(ADD_THREADS) k_add_finish(AddArgs A)
     }
 }
 
+#define ADD_LEAN_THREADS 256
+// k_add_finish for many chains per launch (round 5, the headline's 384): a 4-wave block
+// whose only LDS is the cell start table (uint16, 16 KB); the per-cell fill counters and the
+// cell-sorted candidate list live in the chain's int scratch (free once PnP is done, same
+// stream).  The 16-wave, 128 KB-LDS form needed a CU with nearly all of its LDS free, which
+// under another stream group's LK flood (~4 KB of LDS per wave) meant waiting for a CU to
+// drain (headline 65.7k -> 66.2-66.5k frames/s; at 1-128 chains per launch the
+// 16-wave form is faster, 2-5 %: profiles/r5_add_lean_ab.jsonl).  The result does not depend on the block shape: the grid only narrows which existing
+// candidates a corner is tested against (any one within min_dist rejects it), and the corners
+// are appended in their order by the chunked block scan.
+__global__ void __launch_bounds__(ADD_LEAN_THREADS) k_add_finish_lean(AddArgs A)
+{
+    __shared__ uint16_t cstart[ADD_MAX_CELLS + 1];
+    __shared__ int lds[16];
+    __shared__ int sh_scan[ADD_LEAN_THREADS / 64];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const vo_dims& d = A.d;
+    const vo_state& s = A.s;
+    if (s.status[b] != 0) return;
+    const int nF = s.nF[b];
+    const int M = s.nCorners[b];
+    if (M < 0) { if (tid == 0) s.status[b] = VO_ST_CAPACITY; return; }      // k_gftt_select overflow
+    if (M == 0) { if (tid == 0) s.status[b] = VO_ST_GFTT_NONE; return; }   // None.squeeze()
+    if (M == 1) { if (tid == 0) s.status[b] = VO_ST_GFTT_ONE; return; }    // (2,) indexing
+    const int P = s.nC[b];
+    float* ck = s.c_kp + (int64_t)b * d.pcap * 2;
+    float* cf = s.c_first + (int64_t)b * d.pcap * 2;
+    int32_t* ct = s.c_tau + (int64_t)b * d.pcap;
+    const float* cor = s.corners + (int64_t)b * d.mcap * 2;
+    const float mdf = (float)A.min_dist;
+    // cells of at least minDistance: the 3x3 neighbourhood holds every candidate within it.
+    // Coarser cells keep that exact, so they grow until the grid fits the LDS table.
+    int cs = (int)ceil(A.min_dist) > 0 ? (int)ceil(A.min_dist) : 1;
+    while ((d.W / cs + 3) * (d.H / cs + 3) > ADD_MAX_CELLS) ++cs;
+    const int gw = d.W / cs + 3, gh = d.H / cs + 3;
+    int* cfill = s.iwork + (int64_t)b * d.iwork_stride;                // [ADD_MAX_CELLS]
+    int* items = cfill + ADD_MAX_CELLS;                                 // [P]
+    // the all-pairs test below (O(M * P)) when the list does not fit the scratch or uint16
+    const bool grid = P < 65536 && (int64_t)ADD_MAX_CELLS + P <= d.iwork_stride;
+    if (grid) {
+        const int ncell = gw * gh;
+        for (int q = tid; q < ncell; q += blockDim.x) cfill[q] = 0;
+        __syncthreads();
+        for (int i = tid; i < P; i += blockDim.x) {
+            int cx = (int)floorf(ck[2 * i] / (float)cs) + 1, cy = (int)floorf(ck[2 * i + 1] / (float)cs) + 1;
+            cx = cx < 0 ? 0 : (cx > gw - 1 ? gw - 1 : cx);
+            cy = cy < 0 ? 0 : (cy > gh - 1 ? gh - 1 : cy);
+            atomicAdd(&cfill[cy * gw + cx], 1);
+        }
+        __syncthreads();
+        // exclusive scan of the cell counts (block-wide, sequential chunks per thread)
+        const int per = (ncell + blockDim.x - 1) / blockDim.x;
+        const int q0 = tid * per, q1 = min(q0 + per, ncell);
+        int local = 0;
+        for (int q = q0; q < q1; ++q) local += cfill[q];
+        int incl = local;
+        for (int o = 1; o < 64; o <<= 1) { int v = __shfl_up(incl, o, 64); if (lane_id() >= o) incl += v; }
+        if (lane_id() == 63) sh_scan[wave_id()] = incl;
+        __syncthreads();
+        int wbase = 0;
+        for (int w = 0; w < wave_id(); ++w) wbase += sh_scan[w];
+        int run = wbase + incl - local;
+        for (int q = q0; q < q1; ++q) { const int c = cfill[q]; cstart[q] = (uint16_t)run; run += c; cfill[q] = 0; }
+        if (tid == 0) cstart[ncell] = (uint16_t)P;
+        __syncthreads();
+        for (int i = tid; i < P; i += blockDim.x) {
+            int cx = (int)floorf(ck[2 * i] / (float)cs) + 1, cy = (int)floorf(ck[2 * i + 1] / (float)cs) + 1;
+            cx = cx < 0 ? 0 : (cx > gw - 1 ? gw - 1 : cx);
+            cy = cy < 0 ? 0 : (cy > gh - 1 ? gh - 1 : cy);
+            const int cell = cy * gw + cx;
+            items[cstart[cell] + atomicAdd(&cfill[cell], 1)] = i;
+        }
+        __syncthreads();
+    }
+    int nC = P;
+    for (int base = 0; base < M; base += blockDim.x) {
+        const int j = base + tid;
+        bool keep = false;
+        float x = 0, y = 0;
+        if (j < M) {
+            x = cor[2 * j]; y = cor[2 * j + 1];
+            keep = true;
+            if (grid) {
+                const int cx = (int)floorf(x / (float)cs) + 1, cy = (int)floorf(y / (float)cs) + 1;
+                for (int yy = cy - 1; yy <= cy + 1 && keep; ++yy) {
+                    if (yy < 0 || yy >= gh) continue;
+                    for (int xx = cx - 1; xx <= cx + 1 && keep; ++xx) {
+                        if (xx < 0 || xx >= gw) continue;
+                        const int cell = yy * gw + xx;
+                        for (int q = cstart[cell]; q < cstart[cell + 1]; ++q) {
+                            const int i = items[q];
+                            const float dx = x - ck[2 * i], dy = y - ck[2 * i + 1];
+                            if (!(sqrtf(dx * dx + dy * dy) > mdf)) { keep = false; break; }
+                        }
+                    }
+                }
+            } else {
+                for (int i = 0; i < P && keep; ++i) {
+                    const float dx = x - ck[2 * i], dy = y - ck[2 * i + 1];
+                    if (!(sqrtf(dx * dx + dy * dy) > mdf)) keep = false;
+                }
+            }
+        }
+        __syncthreads();   // all reads of ck in this chunk done before appends
+        int tot;
+        const int pos = nC + block_scan_flag(keep, lds, &tot);
+        if (keep && pos < d.pcap) {
+            ck[2 * pos] = x; ck[2 * pos + 1] = y;
+            cf[2 * pos] = x; cf[2 * pos + 1] = y;
+            ct[pos] = nF;                                             // tau = len(transforms)
+        }
+        nC += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (nC > d.pcap) { s.status[b] = VO_ST_CAPACITY; nC = d.pcap; }
+        s.nC[b] = nC;
+        s.num_pts[(int64_t)b * d.fcap + nF] = s.nInl[b];
+        s.nF[b] = nF + 1;
+    }
+}
+
 // cv2.triangulatePoints over independent (P1, P2, x1, x2) rows
 __global__ void k_tri_points(int n, const double* P1, const double* P2, const float* x1, const float* x2, float* out)
 {
@@ -1476,7 +1598,12 @@ extern "C" int vo_add_corners_finish(const vo_dims* d, const vo_opts* o, const v
     A.s = *s;
     A.min_dist = o->feature_min_dist;
     A.boot = 0;
-    hipLaunchKernelGGL(k_add_finish, dim3(d->B), dim3(ADD_THREADS), 0, VO_STREAM(stream), A);
+    // the lean form from 256 chains per launch (VO_ADD_LEAN=0 / 1 forces it off / on)
+    static const int lean_env = [] { const char* e = getenv("VO_ADD_LEAN"); return e ? atoi(e) : -1; }();
+    if (lean_env >= 0 ? lean_env == 1 : d->B >= 256)
+        hipLaunchKernelGGL(k_add_finish_lean, dim3(d->B), dim3(ADD_LEAN_THREADS), 0, VO_STREAM(stream), A);
+    else
+        hipLaunchKernelGGL(k_add_finish, dim3(d->B), dim3(ADD_THREADS), 0, VO_STREAM(stream), A);
     return hip_rc();
 }
 

@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 STAGE_OF = {"k_lk": "track", "k_lk_w": "track", "k_eig": "gftt", "k_nms": "gftt", "k_eignms": "gftt", "k_gftt_select": "gftt",
-            "k_ingest": "pyr_build", "k_pyrdown": "pyr_build", "k_pyr_level": "pyr_build", "k_pyr_rows": "pyr_build", "k_scharr": "pyr_deriv",
+            "k_ingest": "pyr_build", "k_pyrdown": "pyr_build", "k_pyr_level": "pyr_build", "k_pyr_rows": "pyr_build", "k_pyr_tail": "pyr_build", "k_scharr": "pyr_deriv",
             "k_pnp_ransac": "pnp", "k_pnp_apply": "pnp", "k_pnp_tri": "pnp", "k_pnp_fused": "pnp", "k_triangulate": "triangulate",
             "k_track_compact": "track", "k_add_finish": "add_finish", "k_eig3": "gftt", "k_lk_q": "track",
             "k_bf_prep": "match", "k_bf_mfma": "match", "k_bf_merge": "match", "k_bf_fixup": "match",
