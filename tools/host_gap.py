@@ -57,3 +57,27 @@ for i in range(2, n):
     lat.append((t1 - t0, time.perf_counter() - t0))
 r = np.array(lat[10:]) * 1e6
 print("no marks, median us: step() host %.1f | frame %.1f" % tuple(np.median(r, axis=0)))
+# the same frames replayed from the step hipGraph (step_graph: copy into the bound buffer, replay)
+eng3 = Engine(rend.K, opts, fr.shape[-1], fr.shape[-2], batch=1, device=dev, ncap=16384, pcap=16384, fcap=n + 8)
+eng3.bootstrap(fr[0:1], fr[1:2])
+eng3.capture_step()
+torch.cuda.synchronize()
+lat = []
+for i in range(2, n):
+    t0 = time.perf_counter()
+    eng3.step_graph(fr[i:i + 1])
+    t1 = time.perf_counter()
+    eng3.status_word(in_graph=True)
+    lat.append((t1 - t0, time.perf_counter() - t0))
+r = np.array(lat[10:]) * 1e6
+print("graph, median us: step_graph() host %.1f | frame %.1f" % tuple(np.median(r, axis=0)))
+# replay without the input copy (same frame buffer every time: timing only)
+lat = []
+for i in range(2, n):
+    t0 = time.perf_counter()
+    eng3.replay_step()
+    t1 = time.perf_counter()
+    eng3.status_word(in_graph=True)
+    lat.append((t1 - t0, time.perf_counter() - t0))
+r = np.array(lat[10:]) * 1e6
+print("graph without the copy, median us: replay host %.1f | frame %.1f" % tuple(np.median(r, axis=0)))
