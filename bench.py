@@ -541,11 +541,14 @@ class Headline:
         for e in self.engines:
             e.release_bootstrap()                     # 64 GB per engine; the later legs bootstrap their own
 
-    def step(self, j, marks=None):
+    def step(self, j, marks=None, prefetch=False):
+        """Step j of every group; prefetch: step j + 1's frames are known (they are in HBM), so
+        their pyramid is built during this step (Engine.step next_frames)."""
         f, bd = self.frames, self.bounds
         for g, e in enumerate(self.engines):
             with torch.cuda.stream(self.streams[g]):
-                e.step(f[j, bd[g]:bd[g + 1]], marks=marks if g == 0 else None)
+                nxt = f[j + 1, bd[g]:bd[g + 1]] if prefetch and j + 1 < f.shape[0] else None
+                e.step(f[j, bd[g]:bd[g + 1]], marks=marks if g == 0 else None, next_frames=nxt)
 
     def statuses(self):
         return np.concatenate([e.statuses() for e in self.engines])
@@ -602,8 +605,11 @@ def main():
     hl.release()
     step_all = hl.step
 
+    # every step builds the next step's pyramid while it tracks (the frames are in HBM), except
+    # across the clock: the last warm-up step and the last timed step do not, so the timed
+    # region builds exactly one pyramid per timed step
     for i in range(W_steps):
-        step_all(2 + i)
+        step_all(2 + i, prefetch=i + 1 < W_steps)
     torch.cuda.synchronize()
 
     nst = len(Engine.STAGES)
@@ -615,7 +621,8 @@ def main():
     t_start = time.perf_counter()
     for k in range(K_steps):
         e = ev[k]
-        step_all(2 + W_steps + k, marks=lambda i, end, strm, e=e: e[i][int(end)].record(strm))
+        step_all(2 + W_steps + k, marks=lambda i, end, strm, e=e: e[i][int(end)].record(strm),
+                 prefetch=k + 1 < K_steps)
     host_s = time.perf_counter() - t_start          # launch-side time (no sync inside steps)
     torch.cuda.synchronize()
     barrier()

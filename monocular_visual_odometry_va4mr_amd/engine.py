@@ -245,14 +245,29 @@ class Engine:
 
     STAGES = ("pyr_build", "track", "pnp", "triangulate", "gftt", "add_finish")
 
-    def step(self, frames, marks=None):
+    def step(self, frames, marks=None, next_frames=None):
         """One continuous_operation for every chain (frames: uint8 [B,H,W], any device).
 
         ``marks``: optional callable ``marks(stage_index, end, stream)`` invoked on the
         launching thread right before (end=False) and after (end=True) each stage, with
-        the torch stream that stage runs on (bench.py records HIP events there)."""
+        the torch stream that stage runs on (bench.py records HIP events there).
+
+        ``next_frames``: the following step's frames when they are already known (a sequence
+        in memory).  Their pyramid is then built during this step -- on the side stream, as
+        soon as this step's tracking (the last reader of that pyramid buffer) is issued -- and
+        the next step, given the same frames, starts with tracking.  Same kernels, same bytes;
+        the drop-in class, fed one frame per call, never passes it.  Used up to 16 chains per
+        engine: the prefetch is queued on the side stream behind this step's GFTT, which at a
+        few chains ends early (rank 0 of the 8-GPU sequence plan, 2 x 12 chains: 83.2-84.4k ->
+        88.2-89.7k frames/s predicted) but at 24+ chains ends after the next step would have
+        started (headline 68.2-69.1k -> 63.6-63.9k, 48-chain sequence 36.8-36.9k -> 34.4-34.7k;
+        profiles/r5_prefetch_ab.jsonl).  VO_PREFETCH=0 / 1 forces it off / on."""
         frames = self._frames(frames)
-        self._step_launch(frames, self.prev, marks)
+        nxt = None
+        mode = os.environ.get("VO_PREFETCH", "")
+        if next_frames is not None and (mode == "1" or (mode != "0" and self.B <= 16)):
+            nxt = self._frames(next_frames)
+        self._step_launch(frames, self.prev, marks, nxt=nxt)
         self.prev = 1 - self.prev
 
     def _side_stream(self):
@@ -280,7 +295,7 @@ class Engine:
             self._lat = torch.cuda.Stream(self.device, priority=-1)
         return self._lat
 
-    def _step_launch(self, frames, prev, marks=None, gftt_late=False):
+    def _step_launch(self, frames, prev, marks=None, gftt_late=False, nxt=None):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
         new frame (pyr[cur], der[cur]) -> track(prev) -> PnP + triangulate -> [join] ->
         add_finish.  side: GFTT on the new frame (needs only its pyramid,
@@ -307,9 +322,16 @@ class Engine:
                 marks(i, True, strm)
 
         forked = side.cuda_stream != main.cuda_stream
-        run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
+        # pyramid(cur) built during the previous step (next_frames) for these very frames
+        pre, self._pre = getattr(self, "_pre", None), None
+        if pre is not None:
+            main.wait_event(pre[0])                               # the prefetch wrote pyr[cur]
+        if pre is not None and forked and pre[1] == (frames.data_ptr(), cur) and not gftt_late:
+            run(0, main, lambda: 0)
+        else:
+            run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
         if forked:
-            side.wait_stream(main)                                # pyramid(cur) ready
+            side.wait_stream(main)                                # pyramid(cur) ready, last step's corners consumed
         if not gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         fused = getattr(self, "fuse_pnp_tri", os.environ.get("VO_PNP_TRI_SPLIT") != "1")
@@ -320,6 +342,19 @@ class Engine:
         run(1, main, lambda: track(pd, po, ps, prev, sm))
         if gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
+        ev_corners = None
+        if forked:
+            ev_corners = torch.cuda.Event()
+            ev_corners.record(side)                               # corners ready (before any prefetch)
+        if nxt is not None and forked and not gftt_late:
+            # the next frames' pyramid into pyr[prev] / der[prev], which this step's tracking
+            # (just issued on main) is the last to read
+            side.wait_stream(main)
+            nxt.record_stream(side)                               # keep the frames alive for the side stream
+            self._chk(lib.vo_pyr_build(pd, ps, prev, C.c_void_p(nxt.data_ptr()), self.W * self.H, ss), "vo_pyr_build")
+            ev_pre = torch.cuda.Event()
+            ev_pre.record(side)
+            self._pre = (ev_pre, (nxt.data_ptr(), prev))
         lat = main
         if self._prio_latency() and forked:
             lat = self._latency_stream()
@@ -335,7 +370,7 @@ class Engine:
             run(2, lat, lambda: lib.vo_pnp(pd, po, ps, sl))
             run(3, lat, lambda: lib.vo_triangulate(pd, po, ps, 0, sl))
         if forked:
-            lat.wait_stream(side)                                 # corners ready
+            lat.wait_event(ev_corners)                            # corners ready
         run(5, lat, lambda: lib.vo_add_corners_finish(pd, po, ps, sl))
         if lat is not main:
             main.wait_stream(lat)                                 # the step ends on main
@@ -412,6 +447,9 @@ class Engine:
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync: a chain
         whose SIFT keypoints hit the capacity ends with status VO_ST_CAPACITY."""
+        pre, self._pre = getattr(self, "_pre", None), None
+        if pre is not None:
+            torch.cuda.current_stream(self.device).wait_event(pre[0])     # a pending prefetch
         from .features import bf_knn2_batch, matcher_scratch_bytes
         img0 = self._frames(img0)
         img1 = self._frames(img1)

@@ -193,7 +193,12 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     for j in range(n_steps):
         for g, eng in enumerate(engines):
             with on(g):
-                eng.step(step_frames(j, g))
+                # with the frames laid out in HBM, the next step's pyramid is built during this
+                # step (Engine.step next_frames): tracking then starts each step
+                if cuda and idx_dev is not None and j + 1 < n_steps:
+                    eng.step(step_frames(j, g), next_frames=step_frames(j + 1, g))
+                else:
+                    eng.step(step_frames(j, g))
                 if g in ends.get(j, ()):
                     final_status[g] = torch.where(last_dev[g] == j, eng.t["status"], final_status[g])
     if G > 1 and cuda:
