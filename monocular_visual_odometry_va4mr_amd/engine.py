@@ -348,12 +348,15 @@ class Engine:
             ev_corners.record(side)                               # corners ready (before any prefetch)
         if nxt is not None and forked and not gftt_late:
             # the next frames' pyramid into pyr[prev] / der[prev], which this step's tracking
-            # (just issued on main) is the last to read
-            side.wait_stream(main)
-            nxt.record_stream(side)                               # keep the frames alive for the side stream
-            self._chk(lib.vo_pyr_build(pd, ps, prev, C.c_void_p(nxt.data_ptr()), self.W * self.H, ss), "vo_pyr_build")
+            # (just issued on main) is the last to read.  (On a stream of its own instead of
+            # behind this step's GFTT it was slower: the streams share four hardware queues.)
+            pst = side
+            pst.wait_stream(main)
+            nxt.record_stream(pst)                                # keep the frames alive for that stream
+            self._chk(lib.vo_pyr_build(pd, ps, prev, C.c_void_p(nxt.data_ptr()), self.W * self.H,
+                                       C.c_void_p(pst.cuda_stream)), "vo_pyr_build")
             ev_pre = torch.cuda.Event()
-            ev_pre.record(side)
+            ev_pre.record(pst)
             self._pre = (ev_pre, (nxt.data_ptr(), prev))
         lat = main
         if self._prio_latency() and forked:
