@@ -50,6 +50,7 @@ from monocular_visual_odometry_va4mr_amd import options as Op          # noqa: E
 from monocular_visual_odometry_va4mr_amd.engine import Engine          # noqa: E402
 from monocular_visual_odometry_va4mr_amd.synth import Renderer, poses  # noqa: E402
 from monocular_visual_odometry_va4mr_amd import shards as Sh           # noqa: E402
+from monocular_visual_odometry_va4mr_amd import evaluation as Ev       # noqa: E402
 
 SEQ_LEN = 4541          # KITTI seq00 frame count
 SEQ_OVERLAP = 15        # frames shared by neighbouring shards of the sequence job (--seq-overlap)
@@ -320,10 +321,11 @@ def sequence_leg(device, seed, rank, world, per_gpu=48, groups=None, reps=3, ove
     from monocular_visual_odometry_va4mr_amd.run_sequence import reference_for, run
     n_shards = world * per_gpu
     ref = reference_for(os.path.join(ROOT, "tests", "golden"), n_shards, overlap)
+    rnd = seq_renderer(device, seed)
     runs = []
     for _ in range(reps):
         r = run("kitti", SEQ_LEN, per_gpu, overlap=overlap, seed=seed, device=device, rank=rank, world=world,
-                reference=ref, time_boot=False, groups=groups)
+                reference=ref, time_boot=False, groups=groups, renderer=rnd)
         if r is not None:
             runs.append(r)
         torch.cuda.empty_cache()
@@ -332,6 +334,14 @@ def sequence_leg(device, seed, rank, world, per_gpu=48, groups=None, reps=3, ove
     res = sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2]
     st = res.get("stitched") or {}
     vs = res.get("vs_reference")
+    # the stitched job against the reference class run as one chain over the whole sequence
+    # (informational; rank 0 holds every shard after the gather)
+    one = None
+    p1 = os.path.join(ROOT, "tests", "golden", "kitti_seq00.npz")
+    if os.path.exists(p1) and res.get("_stitched") is not None:
+        g1 = np.load(p1, allow_pickle=False)
+        if int(g1["seed"]) == seed and int(g1["n_frames"]) == SEQ_LEN:
+            one = Ev.stitched_vs_one_chain(res["_stitched"], g1["t"], int(g1["boot"][1]))
     return {"overlap": overlap, "config": f"C2 whole sequence: {SEQ_LEN} frames as {res['shards']} overlapping shards "
                       f"({per_gpu} per GPU, {res['groups']} stream group(s)) on {world} GPU(s), "
                       "bootstrap + every step timed, poses gathered + Sim(3)-stitched after",
@@ -346,45 +356,70 @@ def sequence_leg(device, seed, rank, world, per_gpu=48, groups=None, reps=3, ove
             "failed_shards": res["failed_shards"], "vs_reference": vs,
             "reference_fixture": vs is not None,
             "stitched_frames": st.get("frames"), "coverage_breaks": st.get("coverage_breaks"),
-            "stitched_ate_rel_vs_gt": st.get("ate_rel")}
+            "stitched_ate_rel_vs_gt": st.get("ate_rel"),
+            "stitched_ate_rel_vs_one_chain": one and one["ate_rel"],
+            "stitched_vs_one_chain": one}
 
 
 def rank_slice_leg(device, seed, worlds=(2, 4, 8), reps=3, overlap=SEQ_OVERLAP):
-    """What one rank of an N-GPU sequence job does, measured on this GPU:
-    rank 0's slice of the world = N plan (N x seq_chains_for(N) shards of the C2 sequence; for
-    N = 8, shards 0..31 of the 256-shard cut) run alone, bootstrap included, every shard
-    compared with the reference class's run on the same boundaries.  Ranks hold equal slices
-    and run independently until the final gather, so the job's predicted rate is SEQ_LEN / the
-    rank's wall; `..._incl_stitch` adds the batched stitch of all N x B shards (timed on the
-    reference cut's own poses) -- the RCCL gather of ~0.4 MB is not modelled.  Median of `reps`
-    runs per N, every run's wall listed."""
+    """What the ranks of an N-GPU sequence job do, measured on this GPU:
+    every rank's slice of the world = N plan (N x seq_chains_for(N) shards of the C2 sequence)
+    run alone, one rank after another, bootstrap included, every shard compared with the
+    reference class's run on the same boundaries.  Ranks run independently until the final
+    gather, so the job's wall is the slowest rank's: the predicted rate is SEQ_LEN / max over
+    ranks of the rank's wall (median of `reps` runs per rank); `..._incl_stitch` adds the batched
+    stitch of all N x B shards (timed on the reference cut's own poses) -- the RCCL gather of
+    ~0.4 MB is not modelled.  The frames come from one cached render of the sequence."""
     from monocular_visual_odometry_va4mr_amd.run_sequence import reference_for, run
+    rnd = seq_renderer(device, seed)
     out = {}
     for world in worlds:
         per_gpu = seq_chains_for(world)
         n_shards = world * per_gpu
         ref = reference_for(os.path.join(ROOT, "tests", "golden"), n_shards, overlap)
-        runs = []
-        for _ in range(reps):
-            r = run("kitti", SEQ_LEN, per_gpu, overlap=overlap, seed=seed, device=device, rank=0, world=world,
-                    reference=ref, time_boot=False)
-            runs.append(r)
-            torch.cuda.empty_cache()
-        res = sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2]
+        ranks = []
+        for rank in range(world):
+            runs = []
+            for _ in range(reps):
+                runs.append(run("kitti", SEQ_LEN, per_gpu, overlap=overlap, seed=seed, device=device, rank=rank,
+                                world=world, reference=ref, time_boot=False, renderer=rnd))
+                torch.cuda.empty_cache()
+            ranks.append((sorted(runs, key=lambda r: r["wall_s"])[len(runs) // 2], runs))
+        walls = [res["wall_s"] for res, _ in ranks]
+        worst = int(np.argmax(walls))
+        res0 = ranks[worst][0]
         stitch_ms = stitch_time_ms(ref, n_shards, overlap) if ref else None
-        vs = res.get("vs_reference") or {}
+        vss = [res.get("vs_reference") or {} for res, _ in ranks]
+        cmp_ = [v.get("shards_compared") for v in vss]
+        idt = [v.get("shards_identical") for v in vss]
         out[str(world)] = {
-            "shards_total": n_shards, "rank0_shards": res["shards"], "groups": res["groups"],
-            "per_rank_wall_s": res["wall_s"], "wall_s_runs": [r["wall_s"] for r in runs],
-            "bootstrap_s": res["bootstrap_s"], "steps": res["steps"],
-            "ms_per_step": round(res["step_s"] / max(1, res["steps"]) * 1e3, 4),
-            "predicted_frames_per_s": round(SEQ_LEN / res["wall_s"], 1),
+            "shards_total": n_shards, "shards_per_rank": per_gpu, "groups": res0["groups"],
+            "per_rank_wall_s": walls, "wall_s_runs": [[r["wall_s"] for r in runs] for _, runs in ranks],
+            "slowest_rank": worst, "max_wall_s": walls[worst],
+            "bootstrap_s": [res["bootstrap_s"] for res, _ in ranks], "steps": [res["steps"] for res, _ in ranks],
+            "ms_per_step": [round(res["step_s"] / max(1, res["steps"]) * 1e3, 4) for res, _ in ranks],
+            "predicted_frames_per_s": round(SEQ_LEN / walls[worst], 1),
+            "rank0_predicted_frames_per_s": round(SEQ_LEN / walls[0], 1),
             "stitch_ms_all_shards": stitch_ms,
-            "predicted_frames_per_s_incl_stitch": (round(SEQ_LEN / (res["wall_s"] + stitch_ms * 1e-3), 1)
+            "predicted_frames_per_s_incl_stitch": (round(SEQ_LEN / (walls[worst] + stitch_ms * 1e-3), 1)
                                                    if stitch_ms is not None else None),
-            "shards_ok": res["shards_ok"], "shards_compared": vs.get("shards_compared"),
-            "shards_identical": vs.get("shards_identical")}
+            "shards_ok": int(sum(res["shards_ok"] for res, _ in ranks)),
+            "shards_compared": None if None in cmp_ else int(sum(cmp_)),
+            "shards_identical": None if None in idt else int(sum(idt))}
     return out
+
+
+_SEQ_RENDER = {}
+
+
+def seq_renderer(device, seed):
+    """The C2 sequence rendered once into HBM (SEQ_LEN frames, ~2.1 GB) for every sequence run
+    of this process (the job's frames are pre-rendered before its clock anyway)."""
+    from monocular_visual_odometry_va4mr_amd.synth import CachedRenderer, Renderer
+    key = (str(device), int(seed))
+    if key not in _SEQ_RENDER:
+        _SEQ_RENDER[key] = CachedRenderer(Renderer("kitti", seed=seed, device=device), SEQ_LEN)
+    return _SEQ_RENDER[key]
 
 
 def stitch_time_ms(ref: dict, n_shards: int, overlap: int = 30, iters: int = 5) -> float:
@@ -518,10 +553,13 @@ class Headline:
         self.G = G = max(1, min(G, B))
         self.bounds = [(g * B) // G for g in range(G + 1)]
         self.engines, self.streams = [], []
+        # VO_SHARED_TRACK=1: the groups' tracking launches on one shared stream (Engine.track_stream)
+        shared = torch.cuda.Stream(device) if G > 1 and os.environ.get("VO_SHARED_TRACK") == "1" else None
         for g in range(G):
             self.engines.append(Engine(self.K, opts, self.rend.W, self.rend.H, batch=self.bounds[g + 1] - self.bounds[g],
                                        device=device, ncap=16384, pcap=16384, fcap=n_after + 16))
             self.streams.append(torch.cuda.Stream(device) if G > 1 else torch.cuda.current_stream(device))
+            self.engines[-1].track_stream = shared
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if reserve:

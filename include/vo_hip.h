@@ -120,7 +120,12 @@ typedef struct vo_state {
     uint8_t* pnp_mask;            /* PnP inlier mask [B][ncap]                            */
     double* work;                 /* per-chain fp64 scratch [B][work_stride]              */
     int32_t* iwork;               /* per-chain int scratch  [B][iwork_stride]             */
+    uint64_t* gf_sort;            /* GFTT selection scratch [B][ccap + VO_GF_SORT_EXTRA], zeroed
+                                     at allocation (the split selection leaves it zeroed); NULL
+                                     selects the one-block k_gftt_select                      */
 } vo_state;
+
+#define VO_GF_SORT_EXTRA 4096     /* u64 after the sorted keys: value histogram + counter   */
 
 /* ---- library ---------------------------------------------------------------- */
 const char* vo_version(void);
@@ -132,6 +137,11 @@ int vo_device_cus(void);                          /* compute units of the curren
  * unconstrained forms below).  n > 0 makes those decisions assume n CUs (test hook: every form
  * on a small batch); n = 0 restores the device's own count.  Results never depend on it. */
 int vo_set_launch_cus(int n);
+/* Form of the GFTT corner selection inside vo_gftt (goodFeaturesToTrack's sort + minDistance
+ * walk, VisualOdometryPipeLine.py:256): 0 = automatic (the split one-wave kernels k_gsel_* where
+ * the configuration allows them, else k_gftt_select), 1 = always the one-block k_gftt_select,
+ * 2 = the split form where it applies.  Test / A-B hook; the corner lists are identical. */
+int vo_set_gftt_select(int mode);
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 
@@ -141,6 +151,12 @@ int vo_set_launch_cus(int n);
  * chains.  The derivative buffers' zero border is never written (allocate them zeroed). */
 int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
                  int64_t frame_stride, vo_stream_t stream);
+/* vo_pyr_build with the frames pointer read at run time from *frames_slot (device-readable,
+ * e.g. pinned host memory): a step captured into a hipGraph then takes every frame where it
+ * lies, the caller updating the slot between replays instead of copying the frame into a
+ * captured buffer (Engine.step_graph). */
+int vo_pyr_build_slot(const vo_dims* d, const vo_state* s, int cur, const uint8_t* const* frames_slot,
+                      int64_t frame_stride, vo_stream_t stream);
 /* Scharr derivatives of pyramid `which` into state->der[which] (calcSharrDeriv), border
  * included; vo_pyr_build already produces them, this recomputes them alone. */
 int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t stream);

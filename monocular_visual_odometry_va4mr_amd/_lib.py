@@ -73,8 +73,10 @@ _STATE_FIELDS = [
     "pyr0", "pyr1", "der0", "der1", "lm_X", "lm_kp", "nL", "c_kp", "c_first", "c_tau", "nC",
     "pose_R", "pose_t", "nF", "num_pts", "outl_kp", "inl_kp", "nOutl", "nInl", "status",
     "trk_pts", "trk_st", "trk_err", "eig", "eig_max", "gf_keys", "gf_n", "corners", "nCorners",
-    "pnp_rt", "pnp_ok", "pnp_ninl", "pnp_mask", "work", "iwork",
+    "pnp_rt", "pnp_ok", "pnp_ninl", "pnp_mask", "work", "iwork", "gf_sort",
 ]
+
+VO_GF_SORT_EXTRA = 4096
 
 
 class VoState(C.Structure):
@@ -129,7 +131,9 @@ def _declare(L):
         "vo_device_arch": ([C.c_char_p, C.c_int], C.c_int),
         "vo_device_cus": ([], C.c_int),
         "vo_set_launch_cus": ([C.c_int], C.c_int),
+        "vo_set_gftt_select": ([C.c_int], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
+        "vo_pyr_build_slot": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),
         "vo_track_lk": ([D, O, S, C.c_int, P], C.c_int),

@@ -56,7 +56,19 @@ struct PyrLevelArgs {
     int w, h, pitch;
     int64_t off;
     int level;
+    // level 0 / frame-sourced levels only: when set, the frames pointer is read from here at
+    // run time (a captured hipGraph of the step takes each frame in place: vo_pyr_build_slot)
+    const uint8_t* const* src_slot;
 };
+
+VO_DEV const uint8_t* pyr_src(const PyrLevelArgs& A)
+{
+    // the slot is rewritten by the host between graph replays: a system-scope load (no stale
+    // cached copy of a previous replay's pointer)
+    return A.src_slot ? (const uint8_t*)__hip_atomic_load((const uint8_t**)A.src_slot, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM)
+                      : A.src;
+}
 
 // L0: level 0 (frame bytes; its instantiation carries no source-staging LDS, so more blocks
 // fit per CU).  FSRC (pyrDown levels): the source level is level 0 read straight from the frame
@@ -93,7 +105,7 @@ VO_DEV void pyr_tile(const PyrLevelArgs& A, int px0, int py0)
     // unrolled): the staging is latency-bound otherwise
     constexpr int NPV = (PH * PV_W + 255) / 256;
     if constexpr (L0) {
-        const uint8_t* fr = A.src + (int64_t)b * A.sstride;
+        const uint8_t* fr = pyr_src(A) + (int64_t)b * A.sstride;
         uint32_t v[NPV];
 #pragma unroll
         for (int i = 0; i < NPV; ++i) {
@@ -126,7 +138,7 @@ VO_DEV void pyr_tile(const PyrLevelArgs& A, int px0, int py0)
         if constexpr (FSRC) {
             // staged byte j of row r = level-0 padded column ax0 + j = frame column
             // refl101(ax0 + j - VO_BORDER), frame row refl101(sy0 + r)
-            const uint8_t* fr = A.src + (int64_t)b * A.sstride;
+            const uint8_t* fr = pyr_src(A) + (int64_t)b * A.sstride;
 #pragma unroll
             for (int i = 0; i < NSR; ++i) {
                 const int e = tid + 256 * i;
@@ -332,7 +344,7 @@ VO_DEV void pyr_rows_wave(const PyrLevelArgs& A, int R, int sx, int sy, int b)
         return o;
     };
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(A.src + (int64_t)b * A.sstride), (short)0, (int)A.sstride, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(pyr_src(A) + (int64_t)b * A.sstride), (short)0, (int)A.sstride, 0x00020000);
     uint8_t* dst = A.pyr + (int64_t)b * A.pstride + A.off;
     // write level row y (+ the border rows that mirror it)
     auto put_row = [&](int y, uint32_t v) {
@@ -2189,16 +2201,395 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
     }
 }
 
+// ---------------------------------------------------------------- GFTT selection, split form
+// (round 6).  k_gftt_select is one block per chain holding ~110 KB of LDS (C2) and 8-16 waves;
+// beside the other stream group's LK flood -- one-wave blocks refilling every wave slot the
+// moment it frees -- such a block starts only once a whole CU has drained (headline: 0.7 ms
+// alone, 5-6 ms in the step).  The split form does the same selection in five LK-shaped
+// launches: one-wave blocks, no LDS except the walk's <= 17 KB, so each block starts in the
+// first wave slot that frees.
+//   k_gsel_gate     many waves per chain: quality gate v > quality * max (featureselect.cpp),
+//                   passing keys appended to the chain's list in any order, and a histogram of
+//                   GS_NB value buckets (bucket = (key_max - fkey(v)) >> shift: descending
+//                   value order, ~1/512 octave wide at C5);
+//   k_gsel_scan     one wave per chain: exclusive scan of the histogram (bucket starts);
+//   k_gsel_scatter  many waves per chain: every passing key to its bucket's range;
+//   k_gsel_rank     many waves per chain: a key's final place = its bucket's start + the keys of
+//                   its bucket larger than it (buckets hold ~1-70 keys: 12 at C2, 66 at C5), so
+//                   the list ends fully sorted, descending u64 key = (value desc, then larger
+//                   address first) as k_gftt_select's bitonic sort;
+//   k_gsel_walk     one wave per chain: OpenCV's sequential minDistance walk over the sorted list,
+//                   64 candidates per round (as the wave path of k_gftt_select): the accepted
+//                   corners' cell grid holds each corner's offset inside its cell (no corner
+//                   table), in LDS as u16 cells when they fit 16 KB, else as u64 cells in the
+//                   chain's eigen-map scratch; conflicts between the candidates of one round are
+//                   found through a 128-entry cell hash of lane masks.
+// The corner list is the one k_gftt_select produces (the GFTT parity tests run both forms).
+// The split kernels do not read the chain status for their work (GFTT runs concurrently with
+// PnP, which may change it mid-way, and the kernels must agree on what the histogram holds);
+// only the walk skips writing corners for a chain that is no longer running, as k_gftt_select.
+#define GS_NB 4096
+#define GS_LDS_CELLS 8192
+#define GS_HASH 128
+
+struct SelSplitParams {
+    uint64_t* keys;          // gf_keys [B][ccap]: local maxima (in), then the bucket-grouped keys
+    int32_t* nkeys;          // gf_n [B]: local maxima (in); passing keys (out, as k_gftt_select)
+    const uint32_t* eig_max;
+    double quality;
+    int ccap, W, H;
+    float invW;
+    int want;                // maxCorners, 1 <= want <= mcap
+    double md2;              // minDistance^2
+    int cs, gw, gh;          // cell size cvRound(minDistance), grid
+    uint32_t cs_m;           // ceil(2^32 / cs): x / cs = umulhi(x, cs_m) for x < 2^16
+    float* corners;
+    int32_t* ncorners;
+    int mcap;
+    uint64_t* sorted;        // gf_sort [B][sstride]: sorted keys [ccap] | histogram u32[GS_NB] | npass
+    int64_t sstride;
+    float* ggrid;            // u64 cell grid in the eigen-map scratch (LDS grid unused), 8-byte aligned
+    int64_t gstride;         // floats per chain (W * H)
+    int wpc;                 // waves per chain of gate / scatter / rank
+    const int32_t* chain_status;
+};
+
+VO_DEV uint32_t* gs_hist(const SelSplitParams& P, int b) { return (uint32_t*)(P.sorted + (int64_t)b * P.sstride + P.ccap); }
+VO_DEV int32_t* gs_npass(const SelSplitParams& P, int b) { return (int32_t*)(gs_hist(P, b) + GS_NB); }
+
+// the chain's gate and bucket map: keys >= lo pass; bucket(k) = (kmax - (k >> 32)) >> shift
+VO_DEV bool gs_range(const SelSplitParams& P, int b, uint64_t& lo, uint32_t& kmax, int& shift)
+{
+    kmax = P.eig_max[b];
+    const float thr = (float)((double)fkey_inv(kmax) * P.quality);
+    lo = ((uint64_t)fkey(thr) + 1ull) << 32;
+    shift = 0;
+    if ((uint64_t)kmax < (lo >> 32)) return false;
+    const uint32_t R = kmax - (uint32_t)(lo >> 32);
+    const int bits = R ? 32 - __clz(R) : 0;
+    shift = bits > 12 ? bits - 12 : 0;
+    return true;
+}
+VO_DEV int gs_bucket(uint64_t k, uint32_t kmax, int shift)
+{
+    const int q = (int)((kmax - (uint32_t)(k >> 32)) >> shift);
+    return q < GS_NB - 1 ? q : GS_NB - 1;
+}
+
+__global__ void __launch_bounds__(64) k_gsel_gate(SelSplitParams P)
+{
+    const int b = blockIdx.x / P.wpc, w = blockIdx.x - b * P.wpc;
+    const int nk_all = P.nkeys[b];
+    if (nk_all > P.ccap) return;                         // capacity: the walk reports it
+    uint64_t lo;
+    uint32_t kmax;
+    int sh;
+    if (!gs_range(P, b, lo, kmax, sh)) return;
+    const uint64_t* keys = P.keys + (int64_t)b * P.ccap;
+    uint64_t* pass = P.sorted + (int64_t)b * P.sstride;
+    uint32_t* hist = gs_hist(P, b);
+    int32_t* npass = gs_npass(P, b);
+    const int lane = lane_id();
+    for (int base = w * 256; base < nk_all; base += P.wpc * 256) {
+        uint64_t kk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = base + u * 64 + lane;
+            kk[u] = i < nk_all ? keys[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool on = kk[u] >= lo;                 // 0 (absent) never passes: lo >= 2^32
+            const uint64_t m = __ballot(on);
+            if (m == 0) continue;
+            if (on) __hip_atomic_fetch_add(&hist[gs_bucket(kk[u], kmax, sh)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            int pos = 0;
+            if (lane == leader) pos = atomicAdd(npass, __popcll(m));
+            pos = __shfl(pos, leader, 64) + __popcll(m & ((1ull << lane) - 1ull));
+            if (on) pass[pos] = kk[u];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) k_gsel_scan(SelSplitParams P)
+{
+    const int b = blockIdx.x;
+    uint32_t* hist = gs_hist(P, b);
+    const int lane = lane_id();
+    uint4* h4 = (uint4*)hist + lane * (GS_NB / 256);     // 64 consecutive bins per lane
+    // two passes over the lane's bins (read to sum, re-read to write) keep it at <= 64 VGPRs, so
+    // the wave fits the slot of one finished LK wave
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < GS_NB / 256; ++j) {
+        const uint4 v = h4[j];
+        sum += v.x + v.y + v.z + v.w;
+    }
+    // inclusive wave scan of the lane sums
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (__ballot(sum != 0) == 0) return;                 // nothing passed (or the chain was skipped)
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int j = 0; j < GS_NB / 256; ++j) {
+        const uint4 v = h4[j];
+        uint4 o;
+        o.x = run; run += v.x;
+        o.y = run; run += v.y;
+        o.z = run; run += v.z;
+        o.w = run; run += v.w;
+        h4[j] = o;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_gsel_scatter(SelSplitParams P)
+{
+    const int b = blockIdx.x / P.wpc, w = blockIdx.x - b * P.wpc;
+    const int n = *gs_npass(P, b);
+    if (n == 0) return;
+    uint64_t lo;
+    uint32_t kmax;
+    int sh;
+    gs_range(P, b, lo, kmax, sh);
+    const uint64_t* pass = P.sorted + (int64_t)b * P.sstride;
+    uint32_t* hist = gs_hist(P, b);
+    uint64_t* grouped = P.keys + (int64_t)b * P.ccap;
+    for (int i = w * 64 + lane_id(); i < n; i += P.wpc * 64) {
+        const uint64_t k = pass[i];
+        const uint32_t pos = atomicAdd(&hist[gs_bucket(k, kmax, sh)], 1u);
+        grouped[pos] = k;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_gsel_rank(SelSplitParams P)
+{
+    const int b = blockIdx.x / P.wpc, w = blockIdx.x - b * P.wpc;
+    const int n = *gs_npass(P, b);
+    if (n == 0) return;
+    uint64_t lo;
+    uint32_t kmax;
+    int sh;
+    gs_range(P, b, lo, kmax, sh);
+    const uint32_t* hist = gs_hist(P, b);              // after the scatter: bucket ends
+    const uint64_t* grouped = P.keys + (int64_t)b * P.ccap;
+    uint64_t* sorted = P.sorted + (int64_t)b * P.sstride;
+    for (int i = w * 64 + lane_id(); i < n; i += P.wpc * 64) {
+        const uint64_t k = grouped[i];
+        const int q = gs_bucket(k, kmax, sh);
+        const int st = q ? (int)hist[q - 1] : 0, en = (int)hist[q];
+        int cnt = 0;
+        for (int j = st; j < en; ++j) cnt += grouped[j] > k ? 1 : 0;
+        sorted[st + cnt] = k;
+    }
+}
+
+// grid cells: up to two (LDS u16: one byte each, cs <= 15) or four (L2 u64: 16 bits each)
+// corners, each stored as 1 + its offset inside the cell (ox | oy << 4, resp. << 8)
+template <bool LDSG>
+__global__ void __launch_bounds__(64) k_gsel_walk(SelSplitParams P)
+{
+    __shared__ uint32_t lgrid[LDSG ? GS_LDS_CELLS / 2 : 1];
+    __shared__ uint64_t rhash[GS_HASH];
+    __shared__ uint32_t rxy[64];
+    const int b = blockIdx.x;
+    const int lane = lane_id();
+    // the histogram and the pass counter are this call's; zero them for the next one
+    uint32_t* hist = gs_hist(P, b);
+    int32_t* npass = gs_npass(P, b);
+    const int n = *npass;
+    const int nk_all = P.nkeys[b];
+#pragma unroll
+    for (int j = 0; j < GS_NB / 256; ++j) ((uint4*)hist)[j * 64 + lane] = make_uint4(0, 0, 0, 0);
+    if (P.chain_status[b] != 0) {
+        if (lane == 0) *npass = 0;
+        return;
+    }
+    if (nk_all > P.ccap) {
+        if (lane == 0) { *npass = 0; P.ncorners[b] = -1; }     // capacity: k_add_finish raises it
+        return;
+    }
+    const int cs = P.cs, gw = P.gw, gh = P.gh, ncell = gw * gh;
+    uint64_t* gg = (uint64_t*)(((uintptr_t)(P.ggrid + (int64_t)b * P.gstride) + 7) & ~(uintptr_t)7);
+    if (LDSG) {
+        for (int q = lane; q < (ncell + 1) / 2; q += 64) lgrid[q] = 0;
+    } else {
+        for (int q = lane; q < ncell; q += 64) __hip_atomic_store(&gg[q], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int q = lane; q < GS_HASH; q += 64) rhash[q] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint64_t* sorted = P.sorted + (int64_t)b * P.sstride;
+    float* out = P.corners + (int64_t)b * P.mcap * 2;
+    int nacc = 0;
+    const int limit = P.want;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint64_t knext = lane < n ? sorted[lane] : 0ull;
+    for (int s0 = 0; s0 < n && nacc < limit; s0 += 64) {
+        const int i = s0 + lane;
+        bool tent = i < n;
+        const uint32_t addr = (uint32_t)knext;
+        knext = i + 64 < n ? sorted[i + 64] : 0ull;         // the next round's keys, in flight
+        int y = (int)((float)addr * P.invW);
+        y += ((uint32_t)(y + 1) * (uint32_t)P.W <= addr) ? 1 : 0;
+        y -= ((uint32_t)y * (uint32_t)P.W > addr) ? 1 : 0;
+        const int x = (int)(addr - (uint32_t)y * (uint32_t)P.W);
+        const int xc = (int)__umulhi((uint32_t)x, P.cs_m), yc = (int)__umulhi((uint32_t)y, P.cs_m);
+        const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
+        const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
+        // OpenCV's grid test against the corners accepted so far
+        if (tent) {
+            for (int yy = y1; yy <= y2 && tent; ++yy)
+                for (int xx = x1; xx <= x2 && tent; ++xx) {
+                    const int c = yy * gw + xx;
+                    uint64_t cv;
+                    if (LDSG) cv = (lgrid[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+                    else cv = __hip_atomic_load(&gg[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    constexpr int SB = LDSG ? 8 : 16, OB = LDSG ? 4 : 8;
+                    constexpr uint64_t SM = (1ull << SB) - 1ull, OM = (1ull << OB) - 1ull;
+#pragma unroll
+                    for (int q = 0; q < (LDSG ? 2 : 4); ++q) {
+                        const uint64_t sl = (cv >> (SB * q)) & SM;
+                        if (sl == 0) break;
+                        const int ax = xx * cs + (int)((sl - 1) & OM), ay = yy * cs + (int)((sl - 1) >> OB);
+                        const float ddx = (float)x - (float)ax, ddy = (float)y - (float)ay;
+                        if ((double)(ddx * ddx + ddy * ddy) < P.md2) { tent = false; break; }
+                    }
+                }
+        }
+        const uint64_t tmask = __ballot(tent);
+        if (tmask == 0) continue;
+        // conflicts with earlier candidates of this round: lanes register in a cell hash, each
+        // reads the masks of its 3x3 neighbourhood and tests the (rare) earlier lanes exactly
+        if (tent) {
+            rxy[lane] = (uint32_t)x | ((uint32_t)y << 16);
+            atomicOr((unsigned long long*)&rhash[(yc * gw + xc) & (GS_HASH - 1)], 1ull << lane);
+        }
+        wave_lds_sync();
+        uint64_t conf = 0;
+        if (tent) {
+            uint64_t m = 0;
+            for (int yy = y1; yy <= y2; ++yy)
+                for (int xx = x1; xx <= x2; ++xx) m |= rhash[(yy * gw + xx) & (GS_HASH - 1)];
+            m &= tmask & below;
+            for (; m; m &= m - 1) {
+                const int j = __builtin_ctzll(m);
+                const uint32_t a = rxy[j];
+                const int tx = (int)(a & 0xFFFF), ty = (int)(a >> 16);
+                const int tcx = (int)__umulhi((uint32_t)tx, P.cs_m), tcy = (int)__umulhi((uint32_t)ty, P.cs_m);
+                if (abs(tcx - xc) <= 1 && abs(tcy - yc) <= 1) {
+                    const float ddx = (float)x - (float)tx, ddy = (float)y - (float)ty;
+                    if ((double)(ddx * ddx + ddy * ddy) < P.md2) conf |= 1ull << j;
+                }
+            }
+        }
+        wave_lds_sync();
+        if (tent) rhash[(yc * gw + xc) & (GS_HASH - 1)] = 0;
+        // in-order resolution: a lane with conflicts is accepted iff none of its earlier
+        // conflicting lanes is
+        const uint64_t cm = __ballot(conf != 0);
+        uint64_t amask = tmask & ~cm;
+        for (uint64_t m = cm; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            const uint64_t cj = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)conf, j) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(conf >> 32), j) << 32);
+            if ((cj & amask) == 0) amask |= 1ull << j;
+        }
+        // maxCorners: the first (limit - nacc) accepted lanes
+        int nnew = __popcll(amask);
+        if (nnew > limit - nacc) {
+            uint64_t m = amask, keep = 0;
+            for (int c = 0; c < limit - nacc; ++c) { const uint64_t lb = m & (~m + 1ull); keep |= lb; m ^= lb; }
+            amask = keep;
+            nnew = limit - nacc;
+        }
+        if ((amask >> lane) & 1ull) {
+            const int idx = nacc + __popcll(amask & below);
+            out[2 * idx] = (float)x;
+            out[2 * idx + 1] = (float)y;
+            // into the first free slot of its cell (two lanes of a round may share a cell)
+            const int c = yc * gw + xc;
+            const int ox = x - xc * cs, oy = y - yc * cs;
+            if (LDSG) {
+                const uint32_t code = 1u + ((uint32_t)ox | ((uint32_t)oy << 4));
+                const int hs = 16 * (c & 1);
+                uint32_t cur = lgrid[c >> 1];
+                for (;;) {
+                    const uint32_t cell = (cur >> hs) & 0xFFFFu;
+                    const uint32_t ncell = (cell & 0xFFu) ? (cell | (code << 8)) : (cell | code);
+                    const uint32_t nv = (cur & ~(0xFFFFu << hs)) | (ncell << hs);
+                    const uint32_t prev = atomicCAS(&lgrid[c >> 1], cur, nv);
+                    if (prev == cur) break;
+                    cur = prev;
+                }
+            } else {
+                const uint64_t code = 1ull + ((uint64_t)ox | ((uint64_t)oy << 8));
+                unsigned long long* cp = (unsigned long long*)&gg[c];
+                unsigned long long cur = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (;;) {
+                    int q = 0;
+                    while (q < 3 && ((cur >> (16 * q)) & 0xFFFFull)) ++q;
+                    const unsigned long long nv = cur | (code << (16 * q));
+                    const unsigned long long prev = atomicCAS(cp, cur, nv);
+                    if (prev == cur) break;
+                    cur = prev;
+                }
+            }
+        }
+        nacc += nnew;
+        // one wave: its LDS operations and its returned L2 atomics are complete in issue order;
+        // no memory wait here (a workgroup-scope fence would wait for the next round's key
+        // loads and the corner stores every round)
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        P.ncorners[b] = nacc;
+        P.nkeys[b] = n;
+        *npass = 0;
+    }
+}
+
 }  // namespace
 
 // ======================================================================= host side
 static inline bool hip_ok() { return hipGetLastError() == hipSuccess; }
 #define VO_STREAM(s) ((hipStream_t)(s))
 
+// GFTT selection form (vo_set_gftt_select): 0 = automatic, 1 = k_gftt_select, 2 = k_gsel_*
+static int g_sel_mode = 0;
+extern "C" int vo_set_gftt_select(int mode)
+{
+    if (mode < 0 || mode > 2) return VO_EARG;
+    g_sel_mode = mode;
+    return VO_OK;
+}
+
+static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames, const uint8_t* const* slot,
+                     int64_t frame_stride, vo_stream_t stream);
+
 extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
                             int64_t frame_stride, vo_stream_t stream)
 {
-    if (!d || !s || !frames || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
+    if (!frames) return VO_EARG;
+    return pyr_build(d, s, cur, frames, nullptr, frame_stride, stream);
+}
+
+extern "C" int vo_pyr_build_slot(const vo_dims* d, const vo_state* s, int cur, const uint8_t* const* frames_slot,
+                                 int64_t frame_stride, vo_stream_t stream)
+{
+    if (!frames_slot) return VO_EARG;
+    return pyr_build(d, s, cur, nullptr, frames_slot, frame_stride, stream);
+}
+
+static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames, const uint8_t* const* slot,
+                     int64_t frame_stride, vo_stream_t stream)
+{
+    if (!d || !s || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
     // very few chains (the drop-in class's one): levels 0 and 1 in one launch (k_pyr01; one chain
     // 1,992-2,015 -> 2,029-2,049 frames/s eager).  At 32 chains per launch (the sequence job) the
     // fused kernel's 30 KB of LDS and byte-wise frame staging cost more than the launch saves
@@ -2207,8 +2598,9 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
     const bool fuse01 = d->nlev >= 2 && (p01_env >= 0 ? p01_env == 1 : d->B <= 8);
     if (fuse01) {
         PyrLevelArgs A0, A1;
-        A0.src = frames; A0.sstride = frame_stride; A0.sw = A0.sh = A0.spitch = 0; A0.soff = 0;
+        A0.src = frames; A0.sstride = frame_stride; A0.sw = A0.sh = A0.spitch = 0; A0.soff = 0; A0.src_slot = slot;
         A1.src = frames; A1.sstride = frame_stride; A1.sw = d->lvl_w[0]; A1.sh = d->lvl_h[0]; A1.spitch = 0; A1.soff = 0;
+        A1.src_slot = slot;
         PyrLevelArgs* As[2] = {&A0, &A1};
         for (int l = 0; l < 2; ++l) {
             PyrLevelArgs& A = *As[l];
@@ -2242,7 +2634,7 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
         for (int i = 0; i < T.n; ++i) {
             const int l = ltail + i;
             PyrLevelArgs& A = T.a[i];
-            A.src = s->pyr[cur]; A.sstride = d->pyr_stride;
+            A.src = s->pyr[cur]; A.sstride = d->pyr_stride; A.src_slot = nullptr;
             A.sw = d->lvl_w[l - 1]; A.sh = d->lvl_h[l - 1]; A.spitch = d->lvl_pitch[l - 1]; A.soff = d->lvl_off[l - 1];
             A.pyr = s->pyr[cur]; A.pstride = d->pyr_stride;
             A.der = s->der[cur]; A.dstride = d->der_stride;
@@ -2259,6 +2651,7 @@ extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const 
     const int lend = tail ? ltail : d->nlev;
     for (int l = fuse01 ? 2 : 0; l < lend; ++l) {
         PyrLevelArgs A;
+        A.src_slot = l == 0 ? slot : nullptr;
         if (l == 0) {
             A.src = frames; A.sstride = frame_stride; A.sw = A.sh = A.spitch = 0; A.soff = 0;
         } else {
@@ -2468,6 +2861,50 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
     E.chain_status = s->status;
     E.eig_out = nullptr;
     launch_eig(E, st);
+    {
+        // the split selection (k_gsel_*) where it applies: a minDistance grid of cells cvRound(md)
+        // <= 255 wide, 1 <= maxCorners <= the corner capacity (no capacity truncation to report),
+        // and the grid in LDS (u16 cells: cs <= 15 and two corners per cell at most, i.e.
+        // (cs - 1)(sqrt 6 - sqrt 2) < md, <= GS_LDS_CELLS cells) or in the eigen-map scratch
+        // (u64 cells of four corners: five never fit a cell of side cs - 1 <= md - 0.5)
+        const double md = o->feature_min_dist;
+        const int cs = md >= 1 ? (int)lrint(md) : 0;
+        const int gw = cs ? (d->W + cs - 1) / cs : 0, gh = cs ? (d->H + cs - 1) / cs : 0;
+        const int64_t cells = (int64_t)gw * gh;
+        const int want = o->feature_max_corners;
+        // VO_SEL_WALK_LDS=0 keeps the walk's grid in L2 even where the LDS grid fits (A/B)
+        static const int walk_lds = [] { const char* e = getenv("VO_SEL_WALK_LDS"); return e ? atoi(e) : 0; }();
+        const bool lds_ok = walk_lds && cs >= 1 && cs <= 15 && (cs - 1) * 1.0352761804100830 < md &&
+                            cells <= GS_LDS_CELLS;
+        const bool glb_ok = cs >= 1 && cells * 8 + 4 <= (int64_t)4 * d->W * d->H;
+        const bool ok = s->gf_sort && cs >= 1 && cs <= 255 && want >= 1 && want <= d->mcap && (lds_ok || glb_ok) &&
+                        d->W <= 65535 && d->H <= 65535;
+        static const int env = [] { const char* e = getenv("VO_SEL_SPLIT"); return e ? atoi(e) : -1; }();
+        const int mode = g_sel_mode ? g_sel_mode : (env >= 0 ? (env ? 2 : 1) : 2);
+        if (ok && mode == 2) {
+            SelSplitParams G;
+            G.keys = s->gf_keys; G.nkeys = s->gf_n; G.eig_max = s->eig_max; G.quality = o->feature_quality_level;
+            G.ccap = d->ccap; G.W = d->W; G.H = d->H; G.invW = 1.0f / (float)d->W;
+            G.want = want; G.md2 = md * md; G.cs = cs; G.gw = gw; G.gh = gh;
+            G.cs_m = (uint32_t)(((1ull << 32) + cs - 1) / cs);
+            G.corners = s->corners; G.ncorners = s->nCorners; G.mcap = d->mcap;
+            G.sorted = s->gf_sort; G.sstride = (int64_t)d->ccap + VO_GF_SORT_EXTRA;
+            G.ggrid = s->eig; G.gstride = (int64_t)d->W * d->H;
+            // waves per chain for the gate / scatter / rank: ~4k local maxima per wave at full
+            // capacity (C2: 57, C5: 64); a wave with nothing left returns at once
+            int wpc = d->ccap / 4096;
+            G.wpc = wpc < 4 ? 4 : (wpc > 64 ? 64 : wpc);
+            G.chain_status = s->status;
+            const int nb = d->B * G.wpc;
+            hipLaunchKernelGGL(k_gsel_gate, dim3(nb), dim3(64), 0, st, G);
+            hipLaunchKernelGGL(k_gsel_scan, dim3(d->B), dim3(64), 0, st, G);
+            hipLaunchKernelGGL(k_gsel_scatter, dim3(nb), dim3(64), 0, st, G);
+            hipLaunchKernelGGL(k_gsel_rank, dim3(nb), dim3(64), 0, st, G);
+            if (lds_ok) hipLaunchKernelGGL(k_gsel_walk<true>, dim3(d->B), dim3(64), 0, st, G);
+            else hipLaunchKernelGGL(k_gsel_walk<false>, dim3(d->B), dim3(64), 0, st, G);
+            return hip_ok() ? VO_OK : VO_EHIP;
+        }
+    }
     SelParams S;
     S.keys = s->gf_keys; S.nkeys = s->gf_n; S.ccap = d->ccap; S.W = d->W; S.H = d->H;
     S.eig_max = s->eig_max; S.quality = o->feature_quality_level;

@@ -793,10 +793,13 @@ VO_DEV void pnp_apply_split(const vo_dims& d, const vo_state& s, double* rvec, c
 {
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-    if (s.status[b] != 0) return;
-    const int n = s.nL[b];
+    // every wave reads the status before wave 0 may store VO_ST_CAPACITY below (a
+    // wave reading it late skipped the landmark compaction); the block is whole here
+    const int st0 = s.status[b], n = s.nL[b], ok = success[b];
+    __syncthreads();
+    if (st0 != 0) return;
     if (n < 8) { if (tid == 0) s.status[b] = VO_ST_NOT_ENOUGH_KP; return; }
-    if (!success[b]) { if (tid == 0) s.status[b] = VO_ST_PNP_FAILED; return; }
+    if (!ok) { if (tid == 0) s.status[b] = VO_ST_PNP_FAILED; return; }
     if (w == 0) {
         if (lane == 0) {
             double rv[3], Rwc[9];

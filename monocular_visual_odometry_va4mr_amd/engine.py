@@ -176,6 +176,7 @@ class Engine:
         T["eig_max"] = z(B, dt=torch.int32)
         T["gf_keys"] = z(B, d.ccap, dt=torch.int64)
         T["gf_n"] = z(B, dt=torch.int32)
+        T["gf_sort"] = z(B, d.ccap + L.VO_GF_SORT_EXTRA, dt=torch.int64)
         T["corners"] = z(B, d.mcap, 2, dt=torch.float32)
         T["nCorners"] = z(B, dt=torch.int32)
         T["pnp_rt"] = z(2, B, 3, dt=torch.float64)
@@ -229,10 +230,20 @@ class Engine:
         """Pyramid + Scharr derivatives of `frames` into pyr[which] / der[which] (vo_pyr_build
         always produces both; deriv=True additionally recomputes der[which] by vo_pyr_deriv)."""
         frames = self._frames(frames)
+        self._drain_prefetch()
         self._chk(self.lib.vo_pyr_build(self._pd, self._ps, which, C.c_void_p(frames.data_ptr()),
                                         self.W * self.H, self.stream), "vo_pyr_build")
         if deriv:
             self._chk(self.lib.vo_pyr_deriv(self._pd, self._ps, which, self.stream), "vo_pyr_deriv")
+
+    def _drain_prefetch(self):
+        """Order a pending next-frames pyramid build (step(next_frames=...)) before whatever the
+        caller launches next on the current stream, and drop it: only step() itself may consume
+        it (graph replays, captures and explicit pyramid builds write the same
+        pyramid buffers)."""
+        pre, self._pre = getattr(self, "_pre", None), None
+        if pre is not None:
+            torch.cuda.current_stream(self.device).wait_event(pre[0])
 
     def _frames(self, frames):
         if not isinstance(frames, torch.Tensor):
@@ -295,7 +306,7 @@ class Engine:
             self._lat = torch.cuda.Stream(self.device, priority=-1)
         return self._lat
 
-    def _step_launch(self, frames, prev, marks=None, gftt_late=False, nxt=None):
+    def _step_launch(self, frames, prev, marks=None, gftt_late=False, nxt=None, slot=None):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
         new frame (pyr[cur], der[cur]) -> track(prev) -> PnP + triangulate -> [join] ->
         add_finish.  side: GFTT on the new frame (needs only its pyramid,
@@ -304,7 +315,9 @@ class Engine:
         ``gftt_late``: issue GFTT after tracking (same DAG).  A captured graph then runs the
         tracking branch on the pyramid's queue and GFTT, which has slack, across queues:
         one chain replays ~17 us faster (GFTT first made tracking wait ~33 us for the
-        cross-queue dependency); eager launches keep the plain order."""
+        cross-queue dependency); eager launches keep the plain order.
+        ``slot``: the pyramid reads the frames pointer from this device-readable address at run
+        time (vo_pyr_build_slot; the captured step graph)."""
         cur = 1 - prev
         lib = self.lib
         main = torch.cuda.current_stream(self.device)
@@ -326,8 +339,10 @@ class Engine:
         pre, self._pre = getattr(self, "_pre", None), None
         if pre is not None:
             main.wait_event(pre[0])                               # the prefetch wrote pyr[cur]
-        if pre is not None and forked and pre[1] == (frames.data_ptr(), cur) and not gftt_late:
+        if pre is not None and forked and pre[1] == (frames.data_ptr(), frames._version, cur) and not gftt_late:
             run(0, main, lambda: 0)
+        elif slot is not None:
+            run(0, main, lambda: lib.vo_pyr_build_slot(pd, ps, cur, slot, self.W * self.H, sm))
         else:
             run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
         if forked:
@@ -339,7 +354,16 @@ class Engine:
         # first in each chain's block (one kernel boundary fewer on the step's critical path)
         defer = fused and os.environ.get("VO_COMPACT_IN_TRACK") != "1"      # =1: A/B option
         track = lib.vo_track_lk if defer else lib.vo_track
-        run(1, main, lambda: track(pd, po, ps, prev, sm))
+        ts = getattr(self, "track_stream", None)
+        if ts is not None and forked and slot is None:
+            # tracking on a stream shared by the engines of a batch (track_stream): their LK
+            # launches run one after another instead of side by side, so one group's PnP,
+            # feature adding and next pyramid overlap the other group's tracking
+            ts.wait_stream(main)                                  # pyramid(cur) built
+            run(1, ts, lambda: track(pd, po, ps, prev, C.c_void_p(ts.cuda_stream)))
+            main.wait_stream(ts)
+        else:
+            run(1, main, lambda: track(pd, po, ps, prev, sm))
         if gftt_late:
             run(4, side, lambda: lib.vo_gftt(pd, po, ps, cur, ss))
         ev_corners = None
@@ -353,11 +377,17 @@ class Engine:
             pst = side
             pst.wait_stream(main)
             nxt.record_stream(pst)                                # keep the frames alive for that stream
+            # marked as this step's stage 0 (the build it replaces is the next step's, which
+            # then records an empty stage 0): the per-stage report keeps one build per step
+            if marks is not None:
+                marks(0, False, pst)
             self._chk(lib.vo_pyr_build(pd, ps, prev, C.c_void_p(nxt.data_ptr()), self.W * self.H,
                                        C.c_void_p(pst.cuda_stream)), "vo_pyr_build")
+            if marks is not None:
+                marks(0, True, pst)
             ev_pre = torch.cuda.Event()
             ev_pre.record(pst)
-            self._pre = (ev_pre, (nxt.data_ptr(), prev))
+            self._pre = (ev_pre, (nxt.data_ptr(), nxt._version, prev))
         lat = main
         if self._prio_latency() and forked:
             lat = self._latency_stream()
@@ -379,41 +409,71 @@ class Engine:
             main.wait_stream(lat)                                 # the step ends on main
 
     def capture_step(self):
-        """Capture the two ping-pong variants of the step into hipGraphs; returns a
-        replay function taking a device frame buffer already bound at capture time."""
+        """Capture the two ping-pong variants of the step into hipGraphs.  The graphs read the
+        frames pointer from a pinned host slot per variant (vo_pyr_build_slot), so a replay
+        takes the frames where they lie (step_graph).  Returns the graphs' own frame buffer
+        (host frames are copied there)."""
+        self._drain_prefetch()
+        torch.cuda.synchronize(self.device)            # nothing pending crosses into the capture
         buf = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=self.device)
         self._sw_alloc()
+        slots = torch.zeros(2, dtype=torch.int64).pin_memory()
+        slots[:] = buf.data_ptr()
         graphs = []
         side = torch.cuda.Stream(self.device)
         for prev in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
-                    self._step_launch(buf, prev, gftt_late=True)
+                    self._step_launch(buf, prev, gftt_late=True, slot=C.c_void_p(slots.data_ptr() + 8 * prev))
                     # the status word of chain 0 as the graph's last node, written into pinned
                     # host memory (status_word then only waits)
                     self._sw_write(C.c_void_p(side.cuda_stream))
             graphs.append(g)
         torch.cuda.synchronize(self.device)
-        self._graphs = {"buf": buf, "g": graphs}
+        # per variant: the frames its slot points at (kept alive) and an event after its last
+        # replay (the slot is rewritten only once that replay has read it)
+        self._graphs = {"buf": buf, "g": graphs, "slots": slots, "src": [buf, buf], "ev": [None, None]}
         return buf
 
-    def replay_step(self):
-        g = self._graphs["g"][self.prev]
-        g.replay()
+    def replay_step(self, frames=None):
+        """Replay the captured step on the current stream; ``frames``: a device uint8 [B,H,W]
+        contiguous tensor to read in place (default: the graphs' own buffer)."""
+        self._drain_prefetch()
+        G = self._graphs
+        v = self.prev
+        src = G["buf"] if frames is None else frames
+        if G["src"][v] is not src:
+            if G["ev"][v] is not None:
+                G["ev"][v].synchronize()                  # that replay has read the old pointer
+            G["slots"][v] = src.data_ptr()
+            G["src"][v] = src
+        G["g"][v].replay()
+        if frames is not None:
+            frames.record_stream(torch.cuda.current_stream(self.device))
+        ev = G["ev"][v] or torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        G["ev"][v] = ev
         self.prev = 1 - self.prev
 
     def step_graph(self, frames):
-        """Same as step(), replayed from a captured hipGraph (one launch per frame; the
-        frames are copied into the graph's bound input buffer first)."""
+        """Same as step(), replayed from a captured hipGraph (one launch per frame).  Device
+        frames of the engine's shape are read in place through the graph's frame slot; host
+        frames are copied into the graph's buffer first."""
         if not self._graphs:
             self.capture_step()
         buf = self._graphs["buf"]
         if (isinstance(frames, torch.Tensor) and frames.dtype == torch.uint8 and frames.shape == buf.shape
-                and frames.device == buf.device):
-            buf.copy_(frames)                       # device frames: no host-side checks / staging
-        else:
-            buf.copy_(self._frames(frames))
+                and frames.device == buf.device and frames.is_contiguous()):
+            self.replay_step(frames)
+            return
+        if not isinstance(frames, torch.Tensor):
+            frames = torch.as_tensor(np.ascontiguousarray(frames))
+        if frames.dim() == 2:
+            frames = frames.unsqueeze(0)
+        if frames.dtype != torch.uint8 or tuple(frames.shape) != tuple(buf.shape):
+            raise ValueError(f"frames must be uint8 [{self.B},{self.H},{self.W}]")
+        buf.copy_(frames)                           # host -> the graphs' buffer, no staging copy
         self.replay_step()
 
     # ------------------------------------------------------------------ bootstrap
@@ -450,9 +510,7 @@ class Engine:
         vo_sift_batch over both frames of every chain, one vo_bf_knn2_batch over its pairs
         and one vo_ratio_matches; then one vo_bootstrap for all chains.  No host sync: a chain
         whose SIFT keypoints hit the capacity ends with status VO_ST_CAPACITY."""
-        pre, self._pre = getattr(self, "_pre", None), None
-        if pre is not None:
-            torch.cuda.current_stream(self.device).wait_event(pre[0])     # a pending prefetch
+        self._drain_prefetch()
         from .features import bf_knn2_batch, matcher_scratch_bytes
         img0 = self._frames(img0)
         img1 = self._frames(img1)

@@ -109,6 +109,30 @@ def shard_report(shards, centres, gt_positions, stitched=None, reference=None) -
     return out
 
 
+def stitched_vs_one_chain(stitched, one_chain_t, boot1: int) -> dict | None:
+    """The stitched multi-shard trajectory against the reference class run as ONE chain over
+    the whole sequence (tests/golden/kitti_seq00.npz: t_CW of frames boot1, boot1 + 1, ...;
+    SURVEY.md §8e's informational figure): Umeyama Sim(3) ATE over the frames both cover, in
+    the stitched segment that covers most of them, relative to the one chain's path length.
+    The monocular chain drifts in scale and is chaotic, so this measures how far
+    two valid trajectories of the same frames are apart, not an error of either."""
+    if stitched is None:
+        return None
+    ref = np.asarray(one_chain_t, np.float64)
+    pos, seg = stitched.positions, stitched.segment
+    frames = np.arange(boot1, boot1 + len(ref))
+    frames = frames[frames < len(pos)]
+    segs = seg[frames]
+    ids, counts = np.unique(segs[segs >= 0], return_counts=True)
+    if len(ids) == 0:
+        return None
+    keep = frames[segs == ids[np.argmax(counts)]]
+    if len(keep) < 3:
+        return None
+    rmse, rel = ate(pos[keep], ref[keep - boot1])
+    return {"frames": int(len(keep)), "ate_rmse": rmse, "ate_rel": rel}
+
+
 def load_shard_cut(path: str, n_shards: int) -> dict | None:
     """One cut of a shard fixture (tests/golden/kitti_seq00_shards*.npz, written by
     make_long_golden.py from the reference class's own runs): per shard its (start, boot1,

@@ -273,6 +273,7 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
         keep = ~np.isnan(stitched.positions[:, 0])
         np.savetxt(out_path, np.c_[np.nonzero(keep)[0], stitched.segment[keep], stitched.positions[keep]],
                    fmt=["%d", "%d", "%.9f", "%.9f", "%.9f"])
+    out["_stitched"] = stitched
     out["_centres"] = centres
     out["_plan"] = plan
     out["_statuses"] = statuses

@@ -46,3 +46,33 @@ def test_shard_report_on_perfect_shards():
     rep = E.shard_report(sh, centres, gt, st)
     assert all(p["ate_rel"] < 1e-9 for p in rep["shards"])
     assert rep["stitched"]["ate_rel"] < 1e-9 and rep["stitched"]["frames"] == 199
+
+
+def test_stitched_vs_one_chain():
+    """The bench's informational figure: a stitched trajectory equal to the one
+    chain up to Sim(3) scores 0; a drifting one does not; frames outside the one chain's range
+    (before its bootstrap frame, after its stop) are ignored."""
+    P = _gt(300)
+    gt = P[:, :, 3]
+    sh = Sh.plan_shards(300, 4, gap=2, overlap=15)
+    centres = [gt[np.array([s.start] + list(range(s.boot1, s.end)))] * 0.5 for s in sh]
+    st = Sh.stitch(sh, centres)
+    one = gt[2:290] * 2.0 + 3.0                  # t of frames 2 .. 289, another scale / origin
+    r = E.stitched_vs_one_chain(st, one, 2)
+    assert r["frames"] == 288 and r["ate_rel"] < 1e-9
+    drift = one.copy()
+    drift[:, 0] += 50.0 * np.linspace(0, 1, len(one)) ** 2       # a bend no similarity removes
+    assert E.stitched_vs_one_chain(st, drift, 2)["ate_rel"] > 1e-3
+    assert E.stitched_vs_one_chain(None, one, 2) is None
+
+
+def test_cached_renderer_bytes_equal():
+    """CachedRenderer (the bench's one render of the sequence) returns the renderer's bytes."""
+    import torch
+    from monocular_visual_odometry_va4mr_amd.synth import CachedRenderer, Renderer
+    base = Renderer("parking", seed=3)
+    c = CachedRenderer(base, 6, chunk=4)
+    Rs, cs = base.gt_poses(8)
+    ids = [5, 0, 3]
+    assert torch.equal(c.render_batch(ids, Rs[ids], cs[ids]), base.render_batch(ids, Rs[ids], cs[ids]))
+    assert torch.equal(c.render_batch([7], Rs[7:8], cs[7:8]), base.render_batch([7], Rs[7:8], cs[7:8]))

@@ -1,0 +1,131 @@
+"""GFTT corner selection: the split one-wave form (k_gsel_gate / scan / scatter / rank / walk)
+and the one-block k_gftt_select against the oracle's goodFeaturesToTrack
+(featureselect.cpp; VisualOdometryPipeLine.py:256), bit for bit.
+
+vo_set_gftt_select(1 | 2) pins the form; configurations the split form does not take
+(minDistance < 1, a grid too large for the scratch, maxCorners <= 0) fall back to the one-block
+kernel in either mode, and are listed here too so both modes are seen to agree there.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+# (quality, minDistance, maxCorners): LDS grid (md 10, 7), L2 grid (md 5, 2, 1.6), one-block
+# fallback (md 1: the L2 grid does not fit; md 0.5: no grid), maxCorners reached mid-round (300)
+CONFIGS = [(0.1, 10, 1400), (0.01, 10, 1400), (0.05, 7, 500), (0.05, 5.0, 300), (0.01, 2.0, 6000),
+           (0.001, 1.6, 8000), (0.01, 1.0, 3000), (0.02, 0.5, 2000), (0.3, 10, 1400), (0.01, 15, 4000)]
+
+
+@pytest.fixture(scope="module")
+def kitti_frames():
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    fr, K, _, _ = make_sequence("kitti", 6, seed=1)
+    return fr, K
+
+
+@pytest.fixture
+def sel_mode():
+    from monocular_visual_odometry_va4mr_amd import _lib as L
+
+    def set_(m):
+        L.check(L.lib().vo_set_gftt_select(int(m)), "vo_set_gftt_select")
+    yield set_
+    set_(0)
+
+
+def _engine(K, B=1, W=1241, H=376, **kw):
+    from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd import options as O
+    opts, _, _ = O.get("kitti")
+    opts.update(kw)
+    return Engine(K, opts, W, H, batch=B, ncap=1024, pcap=1024, fcap=16)
+
+
+def _corners(eng, b=0):
+    n = int(eng.t["nCorners"][b])
+    return eng.t["corners"][b, :max(n, 0)].cpu().numpy(), n
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("q,md,mc", CONFIGS)
+def test_select_forms_match_oracle(kitti_frames, sel_mode, mode, q, md, mc):
+    from oracle import _olib as O
+    fr, K = kitti_frames
+    sel_mode(mode)
+    eng = _engine(K, feature_quality_level=q, feature_min_dist=md, feature_max_corners=mc)
+    eng.build_pyramid(fr[2], 0)
+    for rep in range(2):                  # the split form leaves its scratch zeroed for the next call
+        assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+        torch.cuda.synchronize()
+        got, n = _corners(eng)
+        ref = O.gftt(fr[2], mc, q, md, 3)
+        assert np.array_equal(got, ref), f"mode {mode} q={q} md={md} mc={mc} call {rep}: {n} vs {len(ref)}"
+
+
+def test_select_many_chains_both_forms(kitti_frames, sel_mode):
+    """Six chains on different frames in one launch, three calls alternating the frames (the
+    histogram / counter / grid scratch of one call must not leak into the next), both forms;
+    every chain's list equals the oracle's, and the passing-key count gf_n agrees."""
+    from oracle import _olib as O
+    fr, K = kitti_frames
+    B = 6
+    eng = _engine(K, B=B)
+    refs, passing = {}, {}
+    for mode in (2, 1):
+        sel_mode(mode)
+        for call in range(3):
+            frames = np.stack([fr[(b + call) % len(fr)] for b in range(B)])
+            eng.build_pyramid(frames, 0)
+            assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+            torch.cuda.synchronize()
+            passing[mode, call] = eng.t["gf_n"].cpu().numpy()
+            for b in range(B):
+                i = (b + call) % len(fr)
+                if i not in refs:
+                    refs[i] = O.gftt(fr[i], 1400, 0.1, 10, 3)
+                got, n = _corners(eng, b)
+                assert np.array_equal(got, refs[i]), f"mode {mode} call {call} chain {b}: {n} vs {len(refs[i])}"
+    for call in range(3):
+        assert np.array_equal(passing[1, call], passing[2, call]), "passing-key counts differ between the forms"
+
+
+def test_select_hd_l2_grid(sel_mode):
+    """C5's configuration (1080p, maxCorners 8192, quality 0.01, minDistance 5: the u64 L2 grid)
+    with the split form, two chains."""
+    from oracle import _olib as O
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    fr, K, _, _ = make_sequence("hd1080", 2, seed=0)
+    sel_mode(2)
+    eng = _engine(K, B=2, W=1920, H=1080, feature_max_corners=8192, feature_quality_level=0.01, feature_min_dist=5)
+    eng.build_pyramid(np.stack([fr[0], fr[1]]), 0)
+    assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+    torch.cuda.synchronize()
+    for b in range(2):
+        got, n = _corners(eng, b)
+        ref = O.gftt(fr[b], 8192, 0.01, 5, 3)
+        assert len(ref) == 8192 and np.array_equal(got, ref), f"chain {b}: {n} vs {len(ref)}"
+
+
+def test_select_flat_and_sparse_frames(kitti_frames, sel_mode):
+    """A flat frame (no positive eigenvalue: no corner) and a frame with a few isolated
+    corners, next to a normal one, in both forms."""
+    from oracle import _olib as O
+    fr, K = kitti_frames
+    flat = np.full_like(fr[0], 77)
+    sparse = np.full_like(fr[0], 40)
+    for (y, x) in [(50, 60), (52, 66), (200, 900), (300, 1200), (120, 400)]:
+        sparse[y:y + 4, x:x + 4] = 220
+    frames = np.stack([flat, sparse, fr[3]])
+    for mode in (1, 2):
+        sel_mode(mode)
+        eng = _engine(K, B=3)
+        eng.build_pyramid(frames, 0)
+        assert eng.lib.vo_gftt(eng._pd, eng._po, eng._ps, 0, eng.stream) == 0
+        torch.cuda.synchronize()
+        for b in range(3):
+            got, n = _corners(eng, b)
+            ref = O.gftt(frames[b], 1400, 0.1, 10, 3)
+            assert np.array_equal(got, ref), f"mode {mode} frame {b}: {n} vs {len(ref)}"

@@ -64,3 +64,48 @@ def test_step_launch_forms_agree(monkeypatch, launch_cus, cus):
         for j, (a, b) in enumerate(zip(ref, runs[f])):
             for k in KEYS:
                 assert np.array_equal(a[k], b[k]), f"{f}: step {j} {k}"
+
+
+def test_prefetch_graph_and_host_frames_mixed():
+    """a pending next-frames pyramid build (step(..., next_frames=...)) followed by a
+    graph replay, a pyramid rebuild or host (numpy) frames must give the state of plain eager
+    steps; the captured step reads device frames in place (frame slot) and host frames through
+    its own buffer."""
+    from monocular_visual_odometry_va4mr_amd import options as Op
+    from monocular_visual_odometry_va4mr_amd.engine import Engine
+    from monocular_visual_odometry_va4mr_amd.synth import make_sequence
+    fr, K, _, _ = make_sequence("kitti", 14, seed=1)
+    opts, _, _ = Op.get("kitti")
+    frames = torch.from_numpy(np.ascontiguousarray(fr)).cuda()
+    starts = [0, 2]
+    f = lambda j: frames[[s + 3 + j for s in starts]].contiguous()
+
+    def fresh():
+        e = Engine(K, opts, 1241, 376, batch=len(starts), ncap=4096, pcap=8192, fcap=16)
+        e.bootstrap(frames[starts], frames[[s + 2 for s in starts]])
+        return e
+
+    ref = fresh()
+    ref_snaps = []
+    for j in range(8):
+        ref.step(f(j))
+        torch.cuda.synchronize()
+        ref_snaps.append({k: ref.t[k].cpu().numpy().copy() for k in KEYS})
+    eng = fresh()
+    eng.capture_step()
+    keep = [f(j) for j in range(8)]          # the same tensors: a prefetch is keyed on them
+    plan = [("eager_next", 1), ("graph", None), ("eager_next", 3), ("eager", None), ("graph_host", None),
+            ("eager_next", 6), ("graph", None), ("eager", None)]
+    for j, (how, nxt) in enumerate(plan):
+        if how == "eager_next":
+            eng.step(keep[j], next_frames=keep[nxt])
+        elif how == "eager":
+            eng.step(keep[j])
+        elif how == "graph":
+            eng.step_graph(keep[j])
+        else:
+            eng.step_graph(keep[j].cpu().numpy())
+        torch.cuda.synchronize()
+        for k in KEYS:
+            assert np.array_equal(ref_snaps[j][k], eng.t[k].cpu().numpy()), f"step {j} ({how}): {k}"
+    assert (ref_snaps[-1]["status"] == 0).all()
