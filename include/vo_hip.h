@@ -151,12 +151,6 @@ int vo_set_gftt_select(int mode);
  * chains.  The derivative buffers' zero border is never written (allocate them zeroed). */
 int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
                  int64_t frame_stride, vo_stream_t stream);
-/* vo_pyr_build with the frames pointer read at run time from *frames_slot (device-readable,
- * e.g. pinned host memory): a step captured into a hipGraph then takes every frame where it
- * lies, the caller updating the slot between replays instead of copying the frame into a
- * captured buffer (Engine.step_graph). */
-int vo_pyr_build_slot(const vo_dims* d, const vo_state* s, int cur, const uint8_t* const* frames_slot,
-                      int64_t frame_stride, vo_stream_t stream);
 /* Scharr derivatives of pyramid `which` into state->der[which] (calcSharrDeriv), border
  * included; vo_pyr_build already produces them, this recomputes them alone. */
 int vo_pyr_deriv(const vo_dims* d, const vo_state* s, int which, vo_stream_t stream);

@@ -13,8 +13,10 @@ Same constructor, methods and public attributes as
 
 The whole hot path runs on the GPU through libvo_hip.so (engine.Engine with one chain);
 state stays in HBM and the attributes are read back on access.  The per-frame step is
-captured once into a pair of hipGraphs (ping-pong pyramids) and replayed for every frame
-(SURVEY.md §8f item 1); ``use_graph=False`` launches the stages one by one instead.  The reference's failure
+launched stage by stage (asynchronous launches overlap the GPU); ``use_graph=True`` captures
+it once into a pair of hipGraphs (ping-pong pyramids) and replays them,
+identical results but not faster on one chain (tools/graph_probe.py: 0.45-0.51 vs 0.44-0.46 ms
+per frame), so eager is the default.  The reference's failure
 conditions raise the same exceptions: ValueError("Not enough keypoints for PnP") (:358),
 ValueError("PnP failed") (:352), and the crashes the reference would hit when
 goodFeaturesToTrack yields 0 / 1 corners (:256-258).
@@ -29,7 +31,7 @@ from .engine import Engine
 
 class VisualOdometryPipeLine:
     def __init__(self, K, options, max_frames: int = 8192, landmark_capacity: int = 16384,
-                 candidate_capacity: int = 16384, device=None, use_graph: bool = True):
+                 candidate_capacity: int = 16384, device=None, use_graph: bool = False):
         self.options = options
         self.K = K
         self.K_inv = np.linalg.inv(K)

@@ -133,7 +133,6 @@ def _declare(L):
         "vo_set_launch_cus": ([C.c_int], C.c_int),
         "vo_set_gftt_select": ([C.c_int], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
-        "vo_pyr_build_slot": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),
         "vo_track_lk": ([D, O, S, C.c_int, P], C.c_int),

@@ -56,19 +56,7 @@ struct PyrLevelArgs {
     int w, h, pitch;
     int64_t off;
     int level;
-    // level 0 / frame-sourced levels only: when set, the frames pointer is read from here at
-    // run time (a captured hipGraph of the step takes each frame in place: vo_pyr_build_slot)
-    const uint8_t* const* src_slot;
 };
-
-VO_DEV const uint8_t* pyr_src(const PyrLevelArgs& A)
-{
-    // the slot is rewritten by the host between graph replays: a system-scope load (no stale
-    // cached copy of a previous replay's pointer)
-    return A.src_slot ? (const uint8_t*)__hip_atomic_load((const uint8_t**)A.src_slot, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_SYSTEM)
-                      : A.src;
-}
 
 // L0: level 0 (frame bytes; its instantiation carries no source-staging LDS, so more blocks
 // fit per CU).  FSRC (pyrDown levels): the source level is level 0 read straight from the frame
@@ -105,7 +93,7 @@ VO_DEV void pyr_tile(const PyrLevelArgs& A, int px0, int py0)
     // unrolled): the staging is latency-bound otherwise
     constexpr int NPV = (PH * PV_W + 255) / 256;
     if constexpr (L0) {
-        const uint8_t* fr = pyr_src(A) + (int64_t)b * A.sstride;
+        const uint8_t* fr = A.src + (int64_t)b * A.sstride;
         uint32_t v[NPV];
 #pragma unroll
         for (int i = 0; i < NPV; ++i) {
@@ -138,7 +126,7 @@ VO_DEV void pyr_tile(const PyrLevelArgs& A, int px0, int py0)
         if constexpr (FSRC) {
             // staged byte j of row r = level-0 padded column ax0 + j = frame column
             // refl101(ax0 + j - VO_BORDER), frame row refl101(sy0 + r)
-            const uint8_t* fr = pyr_src(A) + (int64_t)b * A.sstride;
+            const uint8_t* fr = A.src + (int64_t)b * A.sstride;
 #pragma unroll
             for (int i = 0; i < NSR; ++i) {
                 const int e = tid + 256 * i;
@@ -344,7 +332,7 @@ VO_DEV void pyr_rows_wave(const PyrLevelArgs& A, int R, int sx, int sy, int b)
         return o;
     };
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(pyr_src(A) + (int64_t)b * A.sstride), (short)0, (int)A.sstride, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)(A.src + (int64_t)b * A.sstride), (short)0, (int)A.sstride, 0x00020000);
     uint8_t* dst = A.pyr + (int64_t)b * A.pstride + A.off;
     // write level row y (+ the border rows that mirror it)
     auto put_row = [&](int y, uint32_t v) {
@@ -2206,7 +2194,7 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
 // beside the other stream group's LK flood -- one-wave blocks refilling every wave slot the
 // moment it frees -- such a block starts only once a whole CU has drained (headline: 0.7 ms
 // alone, 5-6 ms in the step).  The split form does the same selection in five LK-shaped
-// launches: one-wave blocks, no LDS except the walk's <= 17 KB, so each block starts in the
+// launches: one-wave blocks, no LDS except the walk's 1.3 KB, so each block starts in the
 // first wave slot that frees.
 //   k_gsel_gate     many waves per chain: quality gate v > quality * max (featureselect.cpp),
 //                   passing keys appended to the chain's list in any order, and a histogram of
@@ -2221,15 +2209,14 @@ __global__ void __launch_bounds__(NT) k_gftt_select(SelParams P)
 //   k_gsel_walk     one wave per chain: OpenCV's sequential minDistance walk over the sorted list,
 //                   64 candidates per round (as the wave path of k_gftt_select): the accepted
 //                   corners' cell grid holds each corner's offset inside its cell (no corner
-//                   table), in LDS as u16 cells when they fit 16 KB, else as u64 cells in the
-//                   chain's eigen-map scratch; conflicts between the candidates of one round are
-//                   found through a 128-entry cell hash of lane masks.
+//                   table), as u64 cells in the chain's eigen-map scratch; conflicts between the
+//                   candidates of one round are found through a 128-entry LDS cell hash of lane
+//                   masks (1.3 KB of LDS).
 // The corner list is the one k_gftt_select produces (the GFTT parity tests run both forms).
 // The split kernels do not read the chain status for their work (GFTT runs concurrently with
 // PnP, which may change it mid-way, and the kernels must agree on what the histogram holds);
 // only the walk skips writing corners for a chain that is no longer running, as k_gftt_select.
 #define GS_NB 4096
-#define GS_LDS_CELLS 8192
 #define GS_HASH 128
 
 struct SelSplitParams {
@@ -2248,7 +2235,7 @@ struct SelSplitParams {
     int mcap;
     uint64_t* sorted;        // gf_sort [B][sstride]: sorted keys [ccap] | histogram u32[GS_NB] | npass
     int64_t sstride;
-    float* ggrid;            // u64 cell grid in the eigen-map scratch (LDS grid unused), 8-byte aligned
+    float* ggrid;            // u64 cell grid in the eigen-map scratch, 8-byte aligned
     int64_t gstride;         // floats per chain (W * H)
     int wpc;                 // waves per chain of gate / scatter / rank
     const int32_t* chain_status;
@@ -2388,12 +2375,14 @@ __global__ void __launch_bounds__(64) k_gsel_rank(SelSplitParams P)
     }
 }
 
-// grid cells: up to two (LDS u16: one byte each, cs <= 15) or four (L2 u64: 16 bits each)
-// corners, each stored as 1 + its offset inside the cell (ox | oy << 4, resp. << 8)
-template <bool LDSG>
+// grid cells (u64 in the chain's eigen-map scratch): up to four corners, each stored as 1 + its
+// offset inside the cell (ox | oy << 8).  Every access to the grid comes from this one wave, so
+// all of them are atomics at workgroup scope (coherent among themselves by the memory model,
+// served by the CU's own XCD instead of the device coherence point).  The grid stays out of
+// LDS on purpose: beside the LK flood a block waits for a CU with that much LDS free (a 12 KB
+// u16 cell table in LDS made the headline's walk 6-10 ms instead of 0.5 ms).
 __global__ void __launch_bounds__(64) k_gsel_walk(SelSplitParams P)
 {
-    __shared__ uint32_t lgrid[LDSG ? GS_LDS_CELLS / 2 : 1];
     __shared__ uint64_t rhash[GS_HASH];
     __shared__ uint32_t rxy[64];
     const int b = blockIdx.x;
@@ -2414,12 +2403,9 @@ __global__ void __launch_bounds__(64) k_gsel_walk(SelSplitParams P)
         return;
     }
     const int cs = P.cs, gw = P.gw, gh = P.gh, ncell = gw * gh;
-    uint64_t* gg = (uint64_t*)(((uintptr_t)(P.ggrid + (int64_t)b * P.gstride) + 7) & ~(uintptr_t)7);
-    if (LDSG) {
-        for (int q = lane; q < (ncell + 1) / 2; q += 64) lgrid[q] = 0;
-    } else {
-        for (int q = lane; q < ncell; q += 64) __hip_atomic_store(&gg[q], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    unsigned long long* gg =
+        (unsigned long long*)(((uintptr_t)(P.ggrid + (int64_t)b * P.gstride) + 7) & ~(uintptr_t)7);
+    for (int q = lane; q < ncell; q += 64) __hip_atomic_store(&gg[q], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (int q = lane; q < GS_HASH; q += 64) rhash[q] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -2442,25 +2428,29 @@ __global__ void __launch_bounds__(64) k_gsel_walk(SelSplitParams P)
         const int xc = (int)__umulhi((uint32_t)x, P.cs_m), yc = (int)__umulhi((uint32_t)y, P.cs_m);
         const int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0);
         const int x2 = min(xc + 1, gw - 1), y2 = min(yc + 1, gh - 1);
-        // OpenCV's grid test against the corners accepted so far
+        // OpenCV's grid test against the corners accepted so far: the (up to) nine cells are
+        // loaded together, then tested
         if (tent) {
-            for (int yy = y1; yy <= y2 && tent; ++yy)
-                for (int xx = x1; xx <= x2 && tent; ++xx) {
-                    const int c = yy * gw + xx;
-                    uint64_t cv;
-                    if (LDSG) cv = (lgrid[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
-                    else cv = __hip_atomic_load(&gg[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    constexpr int SB = LDSG ? 8 : 16, OB = LDSG ? 4 : 8;
-                    constexpr uint64_t SM = (1ull << SB) - 1ull, OM = (1ull << OB) - 1ull;
+            unsigned long long cv[9];
 #pragma unroll
-                    for (int q = 0; q < (LDSG ? 2 : 4); ++q) {
-                        const uint64_t sl = (cv >> (SB * q)) & SM;
-                        if (sl == 0) break;
-                        const int ax = xx * cs + (int)((sl - 1) & OM), ay = yy * cs + (int)((sl - 1) >> OB);
-                        const float ddx = (float)x - (float)ax, ddy = (float)y - (float)ay;
-                        if ((double)(ddx * ddx + ddy * ddy) < P.md2) { tent = false; break; }
-                    }
+            for (int k = 0; k < 9; ++k) {
+                const int yy = y1 + k / 3, xx = x1 + k % 3;
+                cv[k] = (yy <= y2 && xx <= x2)
+                            ? __hip_atomic_load(&gg[yy * gw + xx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                            : 0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const int yy = y1 + k / 3, xx = x1 + k % 3;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t sl = (uint32_t)(cv[k] >> (16 * q)) & 0xFFFFu;
+                    if (sl == 0) break;
+                    const int ax = xx * cs + (int)((sl - 1) & 0xFFu), ay = yy * cs + (int)((sl - 1) >> 8);
+                    const float ddx = (float)x - (float)ax, ddy = (float)y - (float)ay;
+                    if ((double)(ddx * ddx + ddy * ddy) < P.md2) tent = false;
                 }
+            }
         }
         const uint64_t tmask = __ballot(tent);
         if (tmask == 0) continue;
@@ -2512,39 +2502,24 @@ __global__ void __launch_bounds__(64) k_gsel_walk(SelSplitParams P)
             const int idx = nacc + __popcll(amask & below);
             out[2 * idx] = (float)x;
             out[2 * idx + 1] = (float)y;
-            // into the first free slot of its cell (two lanes of a round may share a cell)
-            const int c = yc * gw + xc;
-            const int ox = x - xc * cs, oy = y - yc * cs;
-            if (LDSG) {
-                const uint32_t code = 1u + ((uint32_t)ox | ((uint32_t)oy << 4));
-                const int hs = 16 * (c & 1);
-                uint32_t cur = lgrid[c >> 1];
-                for (;;) {
-                    const uint32_t cell = (cur >> hs) & 0xFFFFu;
-                    const uint32_t ncell = (cell & 0xFFu) ? (cell | (code << 8)) : (cell | code);
-                    const uint32_t nv = (cur & ~(0xFFFFu << hs)) | (ncell << hs);
-                    const uint32_t prev = atomicCAS(&lgrid[c >> 1], cur, nv);
-                    if (prev == cur) break;
-                    cur = prev;
-                }
-            } else {
-                const uint64_t code = 1ull + ((uint64_t)ox | ((uint64_t)oy << 8));
-                unsigned long long* cp = (unsigned long long*)&gg[c];
-                unsigned long long cur = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (;;) {
-                    int q = 0;
-                    while (q < 3 && ((cur >> (16 * q)) & 0xFFFFull)) ++q;
-                    const unsigned long long nv = cur | (code << (16 * q));
-                    const unsigned long long prev = atomicCAS(cp, cur, nv);
-                    if (prev == cur) break;
-                    cur = prev;
-                }
+            // into the first free slot of its cell (two lanes of a round may share a cell); the
+            // CAS returns before the wave goes on, so the next round's loads see it
+            const unsigned long long code = 1ull + ((unsigned long long)(x - xc * cs) | ((unsigned long long)(y - yc * cs) << 8));
+            unsigned long long* cp = &gg[yc * gw + xc];
+            unsigned long long cur = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (;;) {
+                int q = 0;
+                while (q < 3 && ((cur >> (16 * q)) & 0xFFFFull)) ++q;
+                const unsigned long long nv = cur | (code << (16 * q));
+                if (__hip_atomic_compare_exchange_strong(cp, &cur, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP))
+                    break;
             }
         }
         nacc += nnew;
-        // one wave: its LDS operations and its returned L2 atomics are complete in issue order;
-        // no memory wait here (a workgroup-scope fence would wait for the next round's key
-        // loads and the corner stores every round)
+        // one wave: its LDS operations and its returned atomics are complete in issue order; no
+        // memory wait here (a fence would wait for the next round's key loads and the corner
+        // stores every round)
         wave_lds_sync();
     }
     if (lane == 0) {
@@ -2569,27 +2544,10 @@ extern "C" int vo_set_gftt_select(int mode)
     return VO_OK;
 }
 
-static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames, const uint8_t* const* slot,
-                     int64_t frame_stride, vo_stream_t stream);
-
 extern "C" int vo_pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames,
                             int64_t frame_stride, vo_stream_t stream)
 {
-    if (!frames) return VO_EARG;
-    return pyr_build(d, s, cur, frames, nullptr, frame_stride, stream);
-}
-
-extern "C" int vo_pyr_build_slot(const vo_dims* d, const vo_state* s, int cur, const uint8_t* const* frames_slot,
-                                 int64_t frame_stride, vo_stream_t stream)
-{
-    if (!frames_slot) return VO_EARG;
-    return pyr_build(d, s, cur, nullptr, frames_slot, frame_stride, stream);
-}
-
-static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t* frames, const uint8_t* const* slot,
-                     int64_t frame_stride, vo_stream_t stream)
-{
-    if (!d || !s || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
+    if (!d || !s || !frames || cur < 0 || cur > 1 || d->nlev < 1) return VO_EARG;
     // very few chains (the drop-in class's one): levels 0 and 1 in one launch (k_pyr01; one chain
     // 1,992-2,015 -> 2,029-2,049 frames/s eager).  At 32 chains per launch (the sequence job) the
     // fused kernel's 30 KB of LDS and byte-wise frame staging cost more than the launch saves
@@ -2598,9 +2556,8 @@ static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t
     const bool fuse01 = d->nlev >= 2 && (p01_env >= 0 ? p01_env == 1 : d->B <= 8);
     if (fuse01) {
         PyrLevelArgs A0, A1;
-        A0.src = frames; A0.sstride = frame_stride; A0.sw = A0.sh = A0.spitch = 0; A0.soff = 0; A0.src_slot = slot;
+        A0.src = frames; A0.sstride = frame_stride; A0.sw = A0.sh = A0.spitch = 0; A0.soff = 0;
         A1.src = frames; A1.sstride = frame_stride; A1.sw = d->lvl_w[0]; A1.sh = d->lvl_h[0]; A1.spitch = 0; A1.soff = 0;
-        A1.src_slot = slot;
         PyrLevelArgs* As[2] = {&A0, &A1};
         for (int l = 0; l < 2; ++l) {
             PyrLevelArgs& A = *As[l];
@@ -2634,7 +2591,7 @@ static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t
         for (int i = 0; i < T.n; ++i) {
             const int l = ltail + i;
             PyrLevelArgs& A = T.a[i];
-            A.src = s->pyr[cur]; A.sstride = d->pyr_stride; A.src_slot = nullptr;
+            A.src = s->pyr[cur]; A.sstride = d->pyr_stride;
             A.sw = d->lvl_w[l - 1]; A.sh = d->lvl_h[l - 1]; A.spitch = d->lvl_pitch[l - 1]; A.soff = d->lvl_off[l - 1];
             A.pyr = s->pyr[cur]; A.pstride = d->pyr_stride;
             A.der = s->der[cur]; A.dstride = d->der_stride;
@@ -2651,7 +2608,6 @@ static int pyr_build(const vo_dims* d, const vo_state* s, int cur, const uint8_t
     const int lend = tail ? ltail : d->nlev;
     for (int l = fuse01 ? 2 : 0; l < lend; ++l) {
         PyrLevelArgs A;
-        A.src_slot = l == 0 ? slot : nullptr;
         if (l == 0) {
             A.src = frames; A.sstride = frame_stride; A.sw = A.sh = A.spitch = 0; A.soff = 0;
         } else {
@@ -2863,24 +2819,23 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
     launch_eig(E, st);
     {
         // the split selection (k_gsel_*) where it applies: a minDistance grid of cells cvRound(md)
-        // <= 255 wide, 1 <= maxCorners <= the corner capacity (no capacity truncation to report),
-        // and the grid in LDS (u16 cells: cs <= 15 and two corners per cell at most, i.e.
-        // (cs - 1)(sqrt 6 - sqrt 2) < md, <= GS_LDS_CELLS cells) or in the eigen-map scratch
-        // (u64 cells of four corners: five never fit a cell of side cs - 1 <= md - 0.5)
+        // <= 255 wide (u64 cells of four corners: five never fit a cell of side cs - 1 <=
+        // md - 0.5) that fits the eigen-map scratch, and 1 <= maxCorners <= the corner capacity
+        // (no capacity truncation to report)
         const double md = o->feature_min_dist;
         const int cs = md >= 1 ? (int)lrint(md) : 0;
         const int gw = cs ? (d->W + cs - 1) / cs : 0, gh = cs ? (d->H + cs - 1) / cs : 0;
         const int64_t cells = (int64_t)gw * gh;
         const int want = o->feature_max_corners;
-        // VO_SEL_WALK_LDS=0 keeps the walk's grid in L2 even where the LDS grid fits (A/B)
-        static const int walk_lds = [] { const char* e = getenv("VO_SEL_WALK_LDS"); return e ? atoi(e) : 0; }();
-        const bool lds_ok = walk_lds && cs >= 1 && cs <= 15 && (cs - 1) * 1.0352761804100830 < md &&
-                            cells <= GS_LDS_CELLS;
-        const bool glb_ok = cs >= 1 && cells * 8 + 4 <= (int64_t)4 * d->W * d->H;
-        const bool ok = s->gf_sort && cs >= 1 && cs <= 255 && want >= 1 && want <= d->mcap && (lds_ok || glb_ok) &&
-                        d->W <= 65535 && d->H <= 65535;
+        const bool ok = s->gf_sort && cs >= 1 && cs <= 255 && cells * 8 + 4 <= (int64_t)4 * d->W * d->H && want >= 1 &&
+                        want <= d->mcap && d->W <= 65535 && d->H <= 65535;
         static const int env = [] { const char* e = getenv("VO_SEL_SPLIT"); return e ? atoi(e) : -1; }();
-        const int mode = g_sel_mode ? g_sel_mode : (env >= 0 ? (env ? 2 : 1) : 2);
+        // automatic: the split form for more than 64 chains per launch, where the one-block
+        // kernel waits for whole CUs beside the other stream group's LK flood (headline 384: the
+        // GFTT stage 5.7 -> 1.9 ms; C5 128: 9.7k -> 10.2k frames/s); at 1-48 chains the GPU has
+        // room for the fat block and its 512-1024 threads finish the walk sooner (one chain
+        // 2,251 vs 2,213 frames/s; the 8-GPU slice of 2 x 12 chains 88.2k vs 82.7k predicted)
+        const int mode = g_sel_mode ? g_sel_mode : (env >= 0 ? (env ? 2 : 1) : (d->B > 64 ? 2 : 1));
         if (ok && mode == 2) {
             SelSplitParams G;
             G.keys = s->gf_keys; G.nkeys = s->gf_n; G.eig_max = s->eig_max; G.quality = o->feature_quality_level;
@@ -2900,8 +2855,7 @@ extern "C" int vo_gftt(const vo_dims* d, const vo_opts* o, const vo_state* s, in
             hipLaunchKernelGGL(k_gsel_scan, dim3(d->B), dim3(64), 0, st, G);
             hipLaunchKernelGGL(k_gsel_scatter, dim3(nb), dim3(64), 0, st, G);
             hipLaunchKernelGGL(k_gsel_rank, dim3(nb), dim3(64), 0, st, G);
-            if (lds_ok) hipLaunchKernelGGL(k_gsel_walk<true>, dim3(d->B), dim3(64), 0, st, G);
-            else hipLaunchKernelGGL(k_gsel_walk<false>, dim3(d->B), dim3(64), 0, st, G);
+            hipLaunchKernelGGL(k_gsel_walk, dim3(d->B), dim3(64), 0, st, G);
             return hip_ok() ? VO_OK : VO_EHIP;
         }
     }

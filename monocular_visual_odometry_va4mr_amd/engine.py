@@ -306,7 +306,7 @@ class Engine:
             self._lat = torch.cuda.Stream(self.device, priority=-1)
         return self._lat
 
-    def _step_launch(self, frames, prev, marks=None, gftt_late=False, nxt=None, slot=None):
+    def _step_launch(self, frames, prev, marks=None, gftt_late=False, nxt=None):
         """Stage DAG of one step on two streams.  main: pyramid + Scharr derivatives of the
         new frame (pyr[cur], der[cur]) -> track(prev) -> PnP + triangulate -> [join] ->
         add_finish.  side: GFTT on the new frame (needs only its pyramid,
@@ -315,9 +315,7 @@ class Engine:
         ``gftt_late``: issue GFTT after tracking (same DAG).  A captured graph then runs the
         tracking branch on the pyramid's queue and GFTT, which has slack, across queues:
         one chain replays ~17 us faster (GFTT first made tracking wait ~33 us for the
-        cross-queue dependency); eager launches keep the plain order.
-        ``slot``: the pyramid reads the frames pointer from this device-readable address at run
-        time (vo_pyr_build_slot; the captured step graph)."""
+        cross-queue dependency); eager launches keep the plain order."""
         cur = 1 - prev
         lib = self.lib
         main = torch.cuda.current_stream(self.device)
@@ -341,8 +339,6 @@ class Engine:
             main.wait_event(pre[0])                               # the prefetch wrote pyr[cur]
         if pre is not None and forked and pre[1] == (frames.data_ptr(), frames._version, cur) and not gftt_late:
             run(0, main, lambda: 0)
-        elif slot is not None:
-            run(0, main, lambda: lib.vo_pyr_build_slot(pd, ps, cur, slot, self.W * self.H, sm))
         else:
             run(0, main, lambda: lib.vo_pyr_build(pd, ps, cur, fp, self.W * self.H, sm))
         if forked:
@@ -355,7 +351,7 @@ class Engine:
         defer = fused and os.environ.get("VO_COMPACT_IN_TRACK") != "1"      # =1: A/B option
         track = lib.vo_track_lk if defer else lib.vo_track
         ts = getattr(self, "track_stream", None)
-        if ts is not None and forked and slot is None:
+        if ts is not None and forked and not gftt_late:
             # tracking on a stream shared by the engines of a batch (track_stream): their LK
             # launches run one after another instead of side by side, so one group's PnP,
             # feature adding and next pyramid overlap the other group's tracking
@@ -409,71 +405,51 @@ class Engine:
             main.wait_stream(lat)                                 # the step ends on main
 
     def capture_step(self):
-        """Capture the two ping-pong variants of the step into hipGraphs.  The graphs read the
-        frames pointer from a pinned host slot per variant (vo_pyr_build_slot), so a replay
-        takes the frames where they lie (step_graph).  Returns the graphs' own frame buffer
-        (host frames are copied there)."""
+        """Capture the two ping-pong variants of the step into hipGraphs; returns the device
+        frame buffer bound at capture time (step_graph copies each frame there).  Measured on
+        one chain (tools/graph_probe.py), the replay is not faster than eager launches, which
+        overlap the GPU anyway: the drop-in class steps eagerly by default.  A frames pointer
+        read by the kernels from a pinned host slot instead of the copy cost ~60 us per frame
+        (system-scope reads of host memory) and was dropped (round 6)."""
         self._drain_prefetch()
         torch.cuda.synchronize(self.device)            # nothing pending crosses into the capture
         buf = torch.zeros((self.B, self.H, self.W), dtype=torch.uint8, device=self.device)
         self._sw_alloc()
-        slots = torch.zeros(2, dtype=torch.int64).pin_memory()
-        slots[:] = buf.data_ptr()
         graphs = []
         side = torch.cuda.Stream(self.device)
         for prev in (0, 1):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(side):
                 with torch.cuda.graph(g, stream=side):
-                    self._step_launch(buf, prev, gftt_late=True, slot=C.c_void_p(slots.data_ptr() + 8 * prev))
+                    self._step_launch(buf, prev, gftt_late=True)
                     # the status word of chain 0 as the graph's last node, written into pinned
                     # host memory (status_word then only waits)
                     self._sw_write(C.c_void_p(side.cuda_stream))
             graphs.append(g)
         torch.cuda.synchronize(self.device)
-        # per variant: the frames its slot points at (kept alive) and an event after its last
-        # replay (the slot is rewritten only once that replay has read it)
-        self._graphs = {"buf": buf, "g": graphs, "slots": slots, "src": [buf, buf], "ev": [None, None]}
+        self._graphs = {"buf": buf, "g": graphs}
         return buf
 
-    def replay_step(self, frames=None):
-        """Replay the captured step on the current stream; ``frames``: a device uint8 [B,H,W]
-        contiguous tensor to read in place (default: the graphs' own buffer)."""
+    def replay_step(self):
         self._drain_prefetch()
-        G = self._graphs
-        v = self.prev
-        src = G["buf"] if frames is None else frames
-        if G["src"][v] is not src:
-            if G["ev"][v] is not None:
-                G["ev"][v].synchronize()                  # that replay has read the old pointer
-            G["slots"][v] = src.data_ptr()
-            G["src"][v] = src
-        G["g"][v].replay()
-        if frames is not None:
-            frames.record_stream(torch.cuda.current_stream(self.device))
-        ev = G["ev"][v] or torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        G["ev"][v] = ev
+        g = self._graphs["g"][self.prev]
+        g.replay()
         self.prev = 1 - self.prev
 
     def step_graph(self, frames):
-        """Same as step(), replayed from a captured hipGraph (one launch per frame).  Device
-        frames of the engine's shape are read in place through the graph's frame slot; host
-        frames are copied into the graph's buffer first."""
+        """Same as step(), replayed from a captured hipGraph (one launch per frame; the frames
+        are copied into the graph's bound buffer first: host frames directly, device frames by
+        one device copy)."""
         if not self._graphs:
             self.capture_step()
         buf = self._graphs["buf"]
-        if (isinstance(frames, torch.Tensor) and frames.dtype == torch.uint8 and frames.shape == buf.shape
-                and frames.device == buf.device and frames.is_contiguous()):
-            self.replay_step(frames)
-            return
         if not isinstance(frames, torch.Tensor):
             frames = torch.as_tensor(np.ascontiguousarray(frames))
         if frames.dim() == 2:
             frames = frames.unsqueeze(0)
         if frames.dtype != torch.uint8 or tuple(frames.shape) != tuple(buf.shape):
             raise ValueError(f"frames must be uint8 [{self.B},{self.H},{self.W}]")
-        buf.copy_(frames)                           # host -> the graphs' buffer, no staging copy
+        buf.copy_(frames)
         self.replay_step()
 
     # ------------------------------------------------------------------ bootstrap

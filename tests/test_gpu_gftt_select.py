@@ -13,8 +13,9 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-# (quality, minDistance, maxCorners): LDS grid (md 10, 7), L2 grid (md 5, 2, 1.6), one-block
-# fallback (md 1: the L2 grid does not fit; md 0.5: no grid), maxCorners reached mid-round (300)
+# (quality, minDistance, maxCorners): cells of 15, 10, 7, 5, 2 px (md 15: 3+ corners could share
+# a cell), one-block fallback (md 1: the cell grid does not fit the scratch; md 0.5: no grid),
+# maxCorners reached mid-round (300)
 CONFIGS = [(0.1, 10, 1400), (0.01, 10, 1400), (0.05, 7, 500), (0.05, 5.0, 300), (0.01, 2.0, 6000),
            (0.001, 1.6, 8000), (0.01, 1.0, 3000), (0.02, 0.5, 2000), (0.3, 10, 1400), (0.01, 15, 4000)]
 

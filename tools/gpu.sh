@@ -4,7 +4,8 @@
 #   bash tools/gpu.sh bench  <tag> [bench args]       one bench line -> gpurun_out/<tag>.json
 #   bash tools/gpu.sh ab     <tag> <reps> <A env> <B env> [bench args]
 #                                                     headline A/B alternating two env settings,
-#                                                     e.g. VO_SEL_SPLIT=1 VO_SEL_SPLIT=0
+#                                                     e.g. VO_SEL_SPLIT=1 VO_SEL_SPLIT=0 (AB_ARGS replaces
+#                                                     the default headline-only flags)
 #   bash tools/gpu.sh timeline <tag> [bench args]     per-queue kernel timeline of the headline
 #   bash tools/gpu.sh trace  <tag> [bench args]       kernel-trace stats of a bench run (by grid)
 #   bash tools/gpu.sh pmc    <tag>                    FETCH/WRITE + k_lk_w SQ counter passes
@@ -42,7 +43,7 @@ ab)
   out=$O/${tag}_ab.jsonl; : > $out
   for i in $(seq $reps); do
     for E in "$A" "$B"; do
-      env $E timeout -k 10 300 python -u bench.py $HL --steps 20 --warmup 5 "$@" > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+      env $E timeout -k 10 300 python -u bench.py ${AB_ARGS:-$HL} --steps 20 --warmup 5 "$@" > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
       summ $O/ab.json "$E" | tee -a $out
     done
   done ;;
