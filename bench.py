@@ -90,11 +90,10 @@ def parse():
                          "tests/golden/kitti_seq00_shards*.npz)")
     ap.add_argument("--no-rank-slices", action="store_true",
                     help="skip the one-rank-of-N sequence slices (rank 0 of world 2 / 4 / 8 on this GPU)")
-    # hardware queues: the package sets GPU_MAX_HW_QUEUES=8 at import unless the environment
-    # has a value (monocular_visual_odometry_va4mr_amd/__init__.py); --hw-queues N overrides it
-    # for experiments (set before HIP initialises; <= 32)
+    # hardware queues: the environment's value (HIP's default 4 on the GPU box); --hw-queues N
+    # overrides it for experiments (set before HIP initialises; <= 32)
     ap.add_argument("--hw-queues", type=int, default=0,
-                    help="GPU_MAX_HW_QUEUES for this process (0 = the package's / environment's value)")
+                    help="GPU_MAX_HW_QUEUES for this process (0 = the environment's value)")
     return ap.parse_args()
 
 
@@ -557,12 +556,15 @@ class Headline:
         self.G = G = max(1, min(G, B))
         self.bounds = [(g * B) // G for g in range(G + 1)]
         self.engines, self.streams = [], []
-        # VO_SHARED_TRACK=1: the groups' tracking launches on one shared stream (Engine.track_stream)
-        shared = torch.cuda.Stream(device) if G > 1 and os.environ.get("VO_SHARED_TRACK") == "1" else None
+        # VO_SHARED_TRACK=1: the groups' tracking launches on one shared stream (Engine.track_stream);
+        # =2: the same with the groups' own streams (pyramid, PnP, feature adding) at high priority
+        st_mode = os.environ.get("VO_SHARED_TRACK", "0")
+        shared = torch.cuda.Stream(device) if G > 1 and st_mode in ("1", "2") else None
         for g in range(G):
             self.engines.append(Engine(self.K, opts, self.rend.W, self.rend.H, batch=self.bounds[g + 1] - self.bounds[g],
                                        device=device, ncap=16384, pcap=16384, fcap=n_after + 16))
-            self.streams.append(torch.cuda.Stream(device) if G > 1 else torch.cuda.current_stream(device))
+            self.streams.append(torch.cuda.Stream(device, priority=-1 if st_mode == "2" else 0) if G > 1
+                                else torch.cuda.current_stream(device))
             self.engines[-1].track_stream = shared
         torch.cuda.synchronize()
         t0 = time.perf_counter()

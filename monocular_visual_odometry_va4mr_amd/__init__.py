@@ -2,13 +2,8 @@
 ManuelWendl/Monocular_Visual_Odometry_VA4MR's VisualOdometryPipeLine as HIP kernels for gfx950
 behind a C ABI (include/vo_hip.h).  Entry points: ``VisualOdometryPipeLine`` (the reference
 class's surface), ``cv2compat`` (its nine cv2 calls), ``engine.Engine`` (batched chains)."""
-import os as _os
-
-# Hardware queues per process.  HIP's default of 4 lets the queue a stream lands on depend on
-# the process's stream history (streams share queues round robin): a process that had captured
-# one hipGraph ran the 64-shard sequence job at 25.7-25.9k instead of 29.6k frames/s; with 8
-# queues the dependence is gone and every measured workload ran equal or faster
-# (profiles/r4_hw_queues.txt).  HIP reads the variable when it initialises, so this takes effect
-# when the package is imported before the process's first HIP call; a value already in the
-# environment is kept (INTEGRATION.md §4).
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues per process: the package leaves GPU_MAX_HW_QUEUES alone (ADVICE r5: importing it
+# used to set 8).  Every launch-shape and stream threshold was measured on the GPU box, whose
+# environment exports HIP's default of 4, and at the round-6 headline 8 queues were not faster
+# (68.3k / 67.7k vs 68.8k / 68.8k frames/s alternating, profiles/r6/hwq_groups_ab.jsonl);
+# bench.py --hw-queues N sets it for experiments.

@@ -6,6 +6,7 @@
 #                                                     headline A/B alternating two env settings,
 #                                                     e.g. VO_SEL_SPLIT=1 VO_SEL_SPLIT=0 (AB_ARGS replaces
 #                                                     the default headline-only flags)
+#   bash tools/gpu.sh abargs <tag> <reps> "<flags A>" "<flags B>"   the same over two bench flag sets
 #   bash tools/gpu.sh timeline <tag> [bench args]     per-queue kernel timeline of the headline
 #   bash tools/gpu.sh trace  <tag> [bench args]       kernel-trace stats of a bench run (by grid)
 #   bash tools/gpu.sh pmc    <tag>                    FETCH/WRITE + k_lk_w SQ counter passes
@@ -45,6 +46,15 @@ ab)
     for E in "$A" "$B"; do
       env $E timeout -k 10 300 python -u bench.py ${AB_ARGS:-$HL} --steps 20 --warmup 5 "$@" > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
       summ $O/ab.json "$E" | tee -a $out
+    done
+  done ;;
+abargs)    # headline A/B alternating two bench flag sets: abargs <tag> <reps> "<flags A>" "<flags B>"
+  reps=$1; A=$2; B=$3; shift 3
+  out=$O/${tag}_ab.jsonl; : > $out
+  for i in $(seq $reps); do
+    for F in "$A" "$B"; do
+      timeout -k 10 300 python -u bench.py ${AB_ARGS:-$HL} --steps 20 --warmup 5 $F > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+      summ $O/ab.json "$F" | tee -a $out
     done
   done ;;
 timeline)
