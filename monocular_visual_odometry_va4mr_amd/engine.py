@@ -267,16 +267,18 @@ class Engine:
         in memory).  Their pyramid is then built during this step -- on the side stream, as
         soon as this step's tracking (the last reader of that pyramid buffer) is issued -- and
         the next step, given the same frames, starts with tracking.  Same kernels, same bytes;
-        the drop-in class, fed one frame per call, never passes it.  Used up to 16 chains per
-        engine: the prefetch is queued on the side stream behind this step's GFTT, which at a
-        few chains ends early (rank 0 of the 8-GPU sequence plan, 2 x 12 chains: 83.2-84.4k ->
-        88.2-89.7k frames/s predicted) but at 24+ chains ends after the next step would have
-        started (headline 68.2-69.1k -> 63.6-63.9k, 48-chain sequence 36.8-36.9k -> 34.4-34.7k;
-        profiles/r5_prefetch_ab.jsonl).  VO_PREFETCH=0 / 1 forces it off / on."""
+        the drop-in class, fed one frame per call, never passes it.  The prefetch is queued on
+        the side stream behind this step's GFTT.  Used up to 16 chains per engine, where GFTT
+        ends early (rank 0 of the 8-GPU sequence plan, 2 x 12 chains: 83.2-84.4k -> 88.2-89.7k
+        frames/s predicted), and from 256 chains, where the split GFTT selection (round 6) ends
+        well inside the step's tracking (headline 67.9-68.7k -> 69.7-70.0k frames/s,
+        profiles/r6/prefetch_ab.jsonl).  At 24 chains GFTT ends after the next step would have
+        started (48-chain sequence 36.9k -> 34.7k, also in round 6); C5's 128 chains per engine
+        are neutral.  VO_PREFETCH=0 / 1 forces it off / on."""
         frames = self._frames(frames)
         nxt = None
         mode = os.environ.get("VO_PREFETCH", "")
-        if next_frames is not None and (mode == "1" or (mode != "0" and self.B <= 16)):
+        if next_frames is not None and (mode == "1" or (mode != "0" and (self.B <= 16 or self.B >= 256))):
             nxt = self._frames(next_frames)
         self._step_launch(frames, self.prev, marks, nxt=nxt)
         self.prev = 1 - self.prev

@@ -48,6 +48,15 @@ ab)
       summ $O/ab.json "$E" | tee -a $out
     done
   done ;;
+abn)       # headline runs cycling over any number of env settings: abn <tag> <reps> "<env 1>" "<env 2>" ...
+  reps=$1; shift
+  out=$O/${tag}_ab.jsonl; : > $out
+  for i in $(seq $reps); do
+    for E in "$@"; do
+      env $E timeout -k 10 300 python -u bench.py ${AB_ARGS:-$HL} --steps 20 --warmup 5 > $O/ab.json 2> $O/ab.err || { tail -20 $O/ab.err; exit 1; }
+      summ $O/ab.json "$E" | tee -a $out
+    done
+  done ;;
 abargs)    # headline A/B alternating two bench flag sets: abargs <tag> <reps> "<flags A>" "<flags B>"
   reps=$1; A=$2; B=$3; shift 3
   out=$O/${tag}_ab.jsonl; : > $out
@@ -62,6 +71,22 @@ timeline)
   python3 tools/timeline.py $O/tl_$tag > $O/tl_$tag.txt
   rm -f $O/tl_$tag/*kernel_trace.csv.bak
   head -60 $O/tl_$tag.txt ;;
+slab)      # sequence rank slices cycling over env settings: slab <tag> <reps> <W:B:O> "<env 1>" "<env 2>" ...
+  reps=$1; spec=$2; shift 2
+  out=$O/${tag}_slab.jsonl; : > $out
+  for i in $(seq $reps); do
+    for E in "$@"; do
+      env $E timeout -k 10 300 python -u tools/slice_sweep.py $spec --reps 3 2> $O/slab.err | python3 -c "
+import json,sys
+for l in sys.stdin: d=json.loads(l); d['tag']=sys.argv[1]; print(json.dumps(d))" "$E" | tee -a $out || { tail -20 $O/slab.err; exit 1; }
+    done
+  done ;;
+slicetl)   # kernel timeline + by-grid stats of one sequence rank slice: slicetl <tag> <W:B:O>
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/stl_$tag -o run -- python tools/slice_sweep.py ${1:-8:24:15} --reps 1 > $O/stl_$tag.log 2>&1 || exit $?
+  python3 tools/timeline.py $O/stl_$tag 1600 > $O/stl_$tag.txt
+  python3 tools/trace_by_grid.py $O/stl_$tag $O/stl_${tag}_by_grid.csv
+  rm -f $O/stl_$tag/*kernel_trace.csv
+  tail -2 $O/stl_$tag.log; head -25 $O/stl_${tag}_by_grid.csv ;;
 trace)
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$tag -o run -- python bench.py "$@" > $O/prof_$tag.json 2> $O/prof_$tag.err || exit $?
   python3 tools/trace_by_grid.py $O/prof_$tag $O/prof_${tag}_by_grid.csv
