@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include <float.h>
+#include <math.h>
 #include <type_traits>
 
 namespace {
@@ -552,6 +553,10 @@ struct LKParams {
     int win_w, win_h, max_count;
     double eps2;
     float min_eig;
+    // k_lk_w's convergence test decided in f32 where a margin settles it: fl32(ddx^2 + ddy^2)
+    // <= eps2_lo means converged, >= eps2_hi not converged, anything between takes the exact
+    // double test (fill_lk; both infinite when eps2 is too small for the f32 form)
+    float eps2_lo, eps2_hi;
     // point segments: seg0 then seg1 (seg1 used only where its count > seg1_min)
     const float* p0;
     const int32_t* n0;
@@ -630,6 +635,21 @@ VO_DEV int to_sgpr(int v)
 }
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 VO_DEV v2i16 as_v2i16(uint32_t u) { return __builtin_bit_cast(v2i16, u); }
+// v_dot2_i32_i16 (VOP3P) with its accumulator in an SGPR or as the inline constant 0: for a
+// constant accumulator the compiler otherwise emits v_mov + v_dot2c (one VALU more)
+VO_DEV int sdot2_sacc(uint32_t a, uint32_t b, int acc)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(acc));
+    return r;
+}
+VO_DEV int sdot2_0(uint32_t a, uint32_t b)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+VO_DEV uint32_t v2u(v2i16 v) { return __builtin_bit_cast(uint32_t, v); }
 
 VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 {
@@ -924,6 +944,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     // scalar load and its wait per iteration
     double eps2;
     asm volatile("" : "=s"(eps2) : "0"(P.eps2));
+    float eps2_lo, eps2_hi;
+    asm volatile("" : "=s"(eps2_lo) : "0"(P.eps2_lo));
+    asm volatile("" : "=s"(eps2_hi) : "0"(P.eps2_hi));
     // window pixels of a lane: column lane % 16, rows 4 j + s with s = (lane / 32) + 2 (lane / 16
     // % 2), so that a 32-lane half reads rows s and s + 2 (row offsets 0 and 2 * QS = 48 dwords,
     // 16 banks apart: conflict-free) and pixel j sits at the constant offset toff + 4 j QS
@@ -1155,9 +1178,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const v2i16 gxp1 = as_v2i16(__builtin_amdgcn_perm((uint32_t)ixv[3], (uint32_t)ixv[2], 0x05040100u));
                 const v2i16 gyp0 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[1], (uint32_t)iyv[0], 0x05040100u));
                 const v2i16 gyp1 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[3], (uint32_t)iyv[2], 0x05040100u));
-                a11 = __builtin_amdgcn_sdot2(gxp0, gxp0, __builtin_amdgcn_sdot2(gxp1, gxp1, 0, false), false);
-                a12 = __builtin_amdgcn_sdot2(gxp0, gyp0, __builtin_amdgcn_sdot2(gxp1, gyp1, 0, false), false);
-                a22 = __builtin_amdgcn_sdot2(gyp0, gyp0, __builtin_amdgcn_sdot2(gyp1, gyp1, 0, false), false);
+                a11 = __builtin_amdgcn_sdot2(gxp0, gxp0, sdot2_0(v2u(gxp1), v2u(gxp1)), false);
+                a12 = __builtin_amdgcn_sdot2(gxp0, gyp0, sdot2_0(v2u(gxp1), v2u(gyp1)), false);
+                a22 = __builtin_amdgcn_sdot2(gyp0, gyp0, sdot2_0(v2u(gyp1), v2u(gyp1)), false);
                 // one exact 32-bit reduction each unless a lane's partial could overflow the sum
                 const bool twide = __ballot((uint32_t)a11 >= (1u << 25) || (uint32_t)a22 >= (1u << 25) ||
                                             (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
@@ -1171,8 +1194,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     A22 = (float)wave_sum_split(a22) * FLT_SCALE;
                 }
                 float D = A11 * A22 - A12 * A12;
-                const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
-                if (minEig < P.min_eig || D < FLT_EPSILON) {
+                // minEig = (A22 + A11 - sqrtf(t)) / (2 WW WH) against min_eig: the correctly rounded
+                // sqrt and division (~30 VALU) only where the raw v_sqrt_f32 (<= 2 ulp) and a
+                // multiply by the reciprocal cannot settle the comparison.  Their error is below
+                // 2^-21 (s + sum) / (2 WW WH) + 2^-21 |m|, inside the margin mg (exact decision).
+                const float tq = (A11 - A22) * (A11 - A22) + 4.f * A12 * A12;
+                const float sum2 = A22 + A11;
+                const float sa = __builtin_amdgcn_sqrtf(tq);
+                const float inv_n = 1.f / (float)(2 * WW * WH);
+                const float ma = (sum2 - sa) * inv_n;
+                const float mg = __builtin_fmaf(0x1p-20f, (sa + sum2) * inv_n + fabsf(ma), 0x1p-100f);
+                bool reject;
+                if (ma + mg < P.min_eig) reject = true;
+                else if (ma - mg >= P.min_eig) reject = false;
+                else reject = (sum2 - sqrtf(tq)) / (float)(2 * WW * WH) < P.min_eig;
+                if (reject || D < FLT_EPSILON) {
                     if (level == 0) status = 0;
                     break;
                 }
@@ -1228,32 +1264,42 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                             if (decltype(negc)::value) sum -= q >> 24;
                             dd[j] = (uint32_t)((int)sum >> 9);       // |diff| <= 8160: an int16
                         }
-                        // b1 = sum diff * Ix, b2 = sum diff * Iy as int16-pair dot products
-                        const v2i16 d01 = as_v2i16(__builtin_amdgcn_perm(dd[1], dd[0], 0x05040100u));
-                        const v2i16 d23 = as_v2i16(__builtin_amdgcn_perm(dd[3], dd[2], 0x05040100u));
-                        b1 = __builtin_amdgcn_sdot2(d01, gxp0, __builtin_amdgcn_sdot2(d23, gxp1, 0, false), false);
-                        b2 = __builtin_amdgcn_sdot2(d01, gyp0, __builtin_amdgcn_sdot2(d23, gyp1, 0, false), false);
+                        // b1 = sum diff * Ix, b2 = sum diff * Iy as int16-pair dot products, each
+                        // seeded with 2^24 (an SGPR operand): b' = b + 2^24
+                        const uint32_t d01 = __builtin_amdgcn_perm(dd[1], dd[0], 0x05040100u);
+                        const uint32_t d23 = __builtin_amdgcn_perm(dd[3], dd[2], 0x05040100u);
+                        b1 = __builtin_amdgcn_sdot2(as_v2i16(d01), gxp0, sdot2_sacc(d23, v2u(gxp1), 1 << 24), false);
+                        b2 = __builtin_amdgcn_sdot2(as_v2i16(d01), gyp0, sdot2_sacc(d23, v2u(gyp1), 1 << 24), false);
                     };
                     if (neg) mismatch(std::true_type());
                     else mismatch(std::false_type());
-                    const bool wide = __ballot((uint32_t)(b1 + (1 << 24)) >= (1u << 25) ||
-                                               (uint32_t)(b2 + (1 << 24)) >= (1u << 25)) != 0;
+                    // |b| < 2^24 in every lane <=> b' in [0, 2^25): then the 64 seeded partials sum
+                    // exactly in int32 (< 2^31) and the seeds come off as 64 * 2^24 = 2^30
+                    const bool wide = __ballot(max((uint32_t)b1, (uint32_t)b2) >= (1u << 25)) != 0;
                     // int32 -> float and int64 -> float round the same integer identically
                     float fb1, fb2;
                     if (!wide) {
                         wave_sum2_swap(b1, b2);
-                        fb1 = (float)b1 * FLT_SCALE; fb2 = (float)b2 * FLT_SCALE;
+                        fb1 = (float)(b1 - (1 << 30)) * FLT_SCALE; fb2 = (float)(b2 - (1 << 30)) * FLT_SCALE;
                     }
-                    else { fb1 = (float)wave_sum_split(b1) * FLT_SCALE; fb2 = (float)wave_sum_split(b2) * FLT_SCALE; }
+                    else {
+                        fb1 = (float)wave_sum_split(b1 - (1 << 24)) * FLT_SCALE;
+                        fb2 = (float)wave_sum_split(b2 - (1 << 24)) * FLT_SCALE;
+                    }
                     const float ddx = (A12 * fb2 - A22 * fb1) * D;
                     const float ddy = (A12 * fb1 - A11 * fb2) * D;
                     nx += ddx;
                     ny += ddy;
                     ox = nx + hx;
                     oy = ny + hy;
-                    // squares of floats are exact in double, so one fma rounds the same sum
-                    const double dy2 = (double)ddy * ddy;
-                    if (__builtin_fma((double)ddx, (double)ddx, dy2) <= eps2) break;
+                    // squares of floats are exact in double, so one fma rounds the same sum; the
+                    // f32 form decides it outside the margin (P.eps2_lo / eps2_hi, fill_lk)
+                    const float q2 = __builtin_fmaf(ddx, ddx, ddy * ddy);
+                    if (q2 <= eps2_lo) break;
+                    if (!(q2 >= eps2_hi)) {
+                        const double dy2 = (double)ddy * ddy;
+                        if (__builtin_fma((double)ddx, (double)ddx, dy2) <= eps2) break;
+                    }
                     if (it > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
                         ox -= ddx * 0.5f;
                         oy -= ddy * 0.5f;
@@ -2685,6 +2731,16 @@ static void fill_lk(LKParams& P, const vo_dims* d, const vo_opts* o, const vo_st
     P.max_count = mc;
     P.eps2 = eps * eps;
     P.min_eig = (float)o->min_eig;
+    // fl32(ddx^2 + ddy^2) (one rounded square, one fma) is within 2^-23 of the exact sum, plus
+    // 2^-125 absolute near underflow: outside eps2 * (1 -+ 2^-20) it decides the double test
+    // (eps2 >= 2^-100 keeps the absolute part far below the margin)
+    if (P.eps2 >= 0x1p-100 && P.eps2 <= 0x1p100) {
+        P.eps2_lo = nextafterf((float)(P.eps2 * (1. - 0x1p-20)), 0.f);
+        P.eps2_hi = nextafterf((float)(P.eps2 * (1. + 0x1p-20)), INFINITY);
+    } else {
+        P.eps2_lo = -INFINITY;
+        P.eps2_hi = INFINITY;
+    }
 }
 
 static int launch_lk(const LKParams& P, int B, hipStream_t st)
