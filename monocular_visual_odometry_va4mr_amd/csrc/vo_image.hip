@@ -1003,6 +1003,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     auto j_store = [&](const uint32_t (&v)[2][NJR]) {
         const int ln = lane + opaque0();
         const int m = ln & 7;
+        const uint32_t jsel1 = (uint32_t)(jsh + 1) * 0x01010101u + 0x03020100u;   // bytes jsh+1 .. jsh+4
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
             const uint32_t a0 = v[0][k], b0 = v[1][k];
@@ -1014,14 +1015,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 #else
             if (m < QM && r < TH) {
 #endif
+                // row r bytes Wa0..Wa4 = bytes jsh .. jsh + 4 of (a1:a0), row r + 1 likewise Wb: A / C
+                // hold W0..W3, Bv / D hold W1..W4 (byte-select by an SGPR selector, which also
+                // covers jsh + 1 = 4); quad i = (Wa_i, Wa_i+1, Wb_i, Wb_i+1), one permute each
                 const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
-                const uint32_t Bv = jsh == 3 ? a1 : __builtin_amdgcn_alignbyte(a1, a0, jsh + 1);
+                const uint32_t Bv = __builtin_amdgcn_perm(a1, a0, jsel1);
                 const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
-                const uint32_t D = jsh == 3 ? b1 : __builtin_amdgcn_alignbyte(b1, b0, jsh + 1);
-                const uint32_t X = __builtin_amdgcn_perm(Bv, A, 0x05010400u), Y = __builtin_amdgcn_perm(Bv, A, 0x07030602u);
-                const uint32_t Xp = __builtin_amdgcn_perm(D, C, 0x05010400u), Yp = __builtin_amdgcn_perm(D, C, 0x07030602u);
-                QT4[r * QM + m] = make_uint4(__builtin_amdgcn_perm(Xp, X, 0x05040100u), __builtin_amdgcn_perm(Xp, X, 0x07060302u),
-                                             __builtin_amdgcn_perm(Yp, Y, 0x05040100u), __builtin_amdgcn_perm(Yp, Y, 0x07060302u));
+                const uint32_t D = __builtin_amdgcn_perm(b1, b0, jsel1);
+                QT4[r * QM + m] = make_uint4(__builtin_amdgcn_perm(C, A, 0x05040100u), __builtin_amdgcn_perm(C, A, 0x06050201u),
+                                             __builtin_amdgcn_perm(C, A, 0x07060302u), __builtin_amdgcn_perm(D, Bv, 0x07060302u));
             }
         }
         wave_lds_sync();
@@ -1162,12 +1164,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                                           __mul24((int)s[QS], iw10) + __mul24((int)s[QS + 1], iw11), 9);
 #endif
                     const int gx2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x05040100u)), wp1,
-                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x05040100u)), wp0,
-                                                               1 << 13, false), false) >> 14;
+                                        sdot2_sacc(__builtin_amdgcn_perm(d01, d00, 0x05040100u), v2u(wp0), 1 << 13),
+                                        false) >> 14;
                     const int gy2 = __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d11, d10, 0x07060302u)), wp1,
-                                        __builtin_amdgcn_sdot2(as_v2i16(__builtin_amdgcn_perm(d01, d00, 0x07060302u)), wp0,
-                                                               1 << 13, false), false) >> 14;
-                    ival[j] = live[j] ? v : 0;
+                                        sdot2_sacc(__builtin_amdgcn_perm(d01, d00, 0x07060302u), v2u(wp0), 1 << 13),
+                                        false) >> 14;
+                    // a dead slot's I needs no mask: its gradients are zeroed below, so its
+                    // mismatch never reaches b1 / b2 (|J - I| <= 8160 still fits the int16 pair),
+                    // and the level-0 error masks it by live[j]
+                    ival[j] = v;
                     iseed[j] = 256u - ((uint32_t)ival[j] << 9);
                     ixv[j] = live[j] ? gx2 : 0;
                     iyv[j] = live[j] ? gy2 : 0;
@@ -1179,18 +1184,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 const v2i16 gyp0 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[1], (uint32_t)iyv[0], 0x05040100u));
                 const v2i16 gyp1 = as_v2i16(__builtin_amdgcn_perm((uint32_t)iyv[3], (uint32_t)iyv[2], 0x05040100u));
                 a11 = __builtin_amdgcn_sdot2(gxp0, gxp0, sdot2_0(v2u(gxp1), v2u(gxp1)), false);
-                a12 = __builtin_amdgcn_sdot2(gxp0, gyp0, sdot2_0(v2u(gxp1), v2u(gyp1)), false);
+                a12 = __builtin_amdgcn_sdot2(gxp0, gyp0, sdot2_sacc(v2u(gxp1), v2u(gyp1), 1 << 24), false);   // a12 + 2^24
                 a22 = __builtin_amdgcn_sdot2(gyp0, gyp0, sdot2_0(v2u(gyp1), v2u(gyp1)), false);
-                // one exact 32-bit reduction each unless a lane's partial could overflow the sum
-                const bool twide = __ballot((uint32_t)a11 >= (1u << 25) || (uint32_t)a22 >= (1u << 25) ||
-                                            (uint32_t)(a12 + (1 << 25)) >= (1u << 26)) != 0;
+                // one exact 32-bit reduction each when every lane has a11, a22 (>= 0) and the seeded
+                // a12 below 2^25 (|a12| < 2^24): the 64 partials then sum below 2^31 (the a12 seeds
+                // come off as 2^30); otherwise the split sums
+                const bool twide = __ballot(max(max((uint32_t)a11, (uint32_t)a22), (uint32_t)a12) >= (1u << 25)) != 0;
                 const float FLT_SCALE = 1.f / (1 << 20);
                 float A11, A12, A22;
                 if (!twide) {
                     wave_sum3_swap(a11, a22, a12);
-                    A11 = (float)a11 * FLT_SCALE; A12 = (float)a12 * FLT_SCALE; A22 = (float)a22 * FLT_SCALE;
+                    A11 = (float)a11 * FLT_SCALE; A12 = (float)(a12 - (1 << 30)) * FLT_SCALE; A22 = (float)a22 * FLT_SCALE;
                 } else {
-                    A11 = (float)wave_sum_split(a11) * FLT_SCALE; A12 = (float)wave_sum_split(a12) * FLT_SCALE;
+                    A11 = (float)wave_sum_split(a11) * FLT_SCALE; A12 = (float)wave_sum_split(a12 - (1 << 24)) * FLT_SCALE;
                     A22 = (float)wave_sum_split(a22) * FLT_SCALE;
                 }
                 float D = A11 * A22 - A12 * A12;
