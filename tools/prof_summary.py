@@ -24,7 +24,8 @@ STAGE_OF = {"k_lk": "track", "k_lk_w": "track", "k_eig": "gftt", "k_nms": "gftt"
             "k_pnp_ransac": "pnp", "k_pnp_apply": "pnp", "k_pnp_tri": "pnp", "k_pnp_fused": "pnp", "k_triangulate": "triangulate",
             "k_track_compact": "track", "k_add_finish": "add_finish", "k_eig3": "gftt", "k_lk_q": "track",
             "k_bf_prep": "match", "k_bf_mfma": "match", "k_bf_merge": "match", "k_bf_fixup": "match",
-            "k_bf_prep_i8": "match", "k_bf_i8": "match"}
+            "k_bf_prep_i8": "match", "k_bf_i8": "match", "k_add_finish_lean": "add_finish", "k_pyr01": "pyr_build",
+            "k_gsel_gate": "gftt", "k_gsel_scan": "gftt", "k_gsel_scatter": "gftt", "k_gsel_rank": "gftt", "k_gsel_walk": "gftt"}
 
 
 def short(name):
