@@ -142,6 +142,13 @@ int vo_set_launch_cus(int n);
  * the configuration allows them, else k_gftt_select), 1 = always the one-block k_gftt_select,
  * 2 = the split form where it applies.  Test / A-B hook; the corner lists are identical. */
 int vo_set_gftt_select(int mode);
+/* A HIP stream of the current device whose kernels may run on every compute unit except
+ * `reserve` of them (every `stride`-th CU-mask bit from stride - 1, hipExtStreamCreateWithCUMask):
+ * tracking on such a stream leaves those CUs to the one-block-per-chain latency kernels of the
+ * other stream groups (measurement option of the sequence job, VO_TRACK_CU_RESERVE).  The caller
+ * destroys it with vo_stream_destroy. */
+int vo_stream_create_cumask(int reserve, int stride, vo_stream_t* out);
+int vo_stream_destroy(vo_stream_t stream);
 
 /* ---- per-frame step stages (replace VisualOdometryPipeLine.py:326-373) --------- */
 

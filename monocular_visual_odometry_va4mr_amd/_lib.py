@@ -132,6 +132,8 @@ def _declare(L):
         "vo_device_cus": ([], C.c_int),
         "vo_set_launch_cus": ([C.c_int], C.c_int),
         "vo_set_gftt_select": ([C.c_int], C.c_int),
+        "vo_stream_create_cumask": ([C.c_int, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+        "vo_stream_destroy": ([P], C.c_int),
         "vo_pyr_build": ([D, S, C.c_int, P, i64, P], C.c_int),
         "vo_pyr_deriv": ([D, S, C.c_int, P], C.c_int),
         "vo_track": ([D, O, S, C.c_int, P], C.c_int),

@@ -34,3 +34,29 @@ extern "C" int vo_device_arch(char* buf, int len)
     buf[len - 1] = 0;
     return VO_OK;
 }
+
+extern "C" int vo_stream_create_cumask(int reserve, int stride, vo_stream_t* out)
+{
+    if (!out || reserve < 0 || stride < 1) return VO_EARG;
+    const int n = vo_device_cus();
+    if (n <= 0) return VO_EHIP;
+    if ((int64_t)reserve * stride > n) return VO_EARG;
+    uint32_t mask[32];
+    const int words = (n + 31) / 32;
+    if (words > 32) return VO_EARG;
+    memset(mask, 0, sizeof mask);
+    for (int i = 0; i < n; ++i) mask[i >> 5] |= 1u << (i & 31);
+    for (int k = 0; k < reserve; ++k) {
+        const int i = stride - 1 + k * stride;
+        mask[i >> 5] &= ~(1u << (i & 31));
+    }
+    hipStream_t st = nullptr;
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask) != hipSuccess) return VO_EHIP;
+    *out = (vo_stream_t)st;
+    return VO_OK;
+}
+
+extern "C" int vo_stream_destroy(vo_stream_t stream)
+{
+    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? VO_OK : VO_EHIP;
+}

@@ -18,6 +18,7 @@ come from the seeded renderer (synth.py), rendered into device memory before the
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import time
@@ -97,6 +98,18 @@ def run(preset: str, n_frames: int, shards_per_rank: int, overlap: int = 30, see
     prio = os.environ.get("VO_SEQ_PRIO", "0") == "1"
     streams = [torch.cuda.Stream(dev, priority=-1 if (prio and g == 0) else 0) if cuda and G > 1 else None
                for g in range(G)]
+    # VO_TRACK_CU_RESERVE=R[:stride] (measurement option): every group's tracking on one stream
+    # kept off R compute units (vo_stream_create_cumask), which stay free for the one-block-per-
+    # chain PnP / feature-adding / GFTT-selection blocks of the other group
+    cu_res = os.environ.get("VO_TRACK_CU_RESERVE", "")
+    if cuda and G > 1 and cu_res:
+        from . import _lib as L
+        r, _, stride = cu_res.partition(":")
+        h = C.c_void_p()
+        L.check(L.lib().vo_stream_create_cumask(int(r), int(stride or 16), C.byref(h)), "vo_stream_create_cumask")
+        ts = torch.cuda.ExternalStream(h.value, device=dev)
+        for e in engines:
+            e.track_stream = ts
 
     n_steps = max(s.n_steps for s in mine)
     lo = min(s.start for s in mine)
