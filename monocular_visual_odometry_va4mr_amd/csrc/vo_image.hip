@@ -651,6 +651,28 @@ VO_DEV int sdot2_0(uint32_t a, uint32_t b)
 }
 VO_DEV uint32_t v2u(v2i16 v) { return __builtin_bit_cast(uint32_t, v); }
 
+// k_lk_w's bilinear weights w (0 .. 2^14) as an 8 + 7-bit split, bytes in the quad order of its J
+// tile (w00, w10, w01, w11): wlo = w & 255, whi = w >> 8.  From the weights' low halves (the
+// float bit patterns of w + 1.5 * 2^23 carry w in their low bits) two 16-bit packs and a few
+// masks on the scalar unit (~10 SALU; the 7 + 7 form took ~25, and k_lk_w is SALU-bound).
+VO_DEV void pack_w8_halves(uint32_t p0, uint32_t p1, uint32_t& wlo, uint32_t& whi)
+{
+    wlo = (p0 & 0x00ff00ffu) | ((p1 & 0x00ff00ffu) << 8);
+    whi = ((p0 >> 8) & 0x00ff00ffu) | (p1 & 0xff00ff00u);
+}
+// operands in SGPRs (the iteration's weights): the two 16-bit packs as s_pack_ll_b32_b16
+VO_DEV void pack_w8(uint32_t u00, uint32_t u01, uint32_t u10, uint32_t w11, uint32_t& wlo, uint32_t& whi)
+{
+    uint32_t p0, p1;                                         // (w00, w01), (w10, w11)
+    asm("s_pack_ll_b32_b16 %0, %1, %2" : "=s"(p0) : "s"(u00), "s"(u01));
+    asm("s_pack_ll_b32_b16 %0, %1, %2" : "=s"(p1) : "s"(u10), "s"(w11));
+    pack_w8_halves(p0, p1, wlo, whi);
+}
+// any operands (the level-0 error pass)
+VO_DEV void pack_w8_v(uint32_t w00, uint32_t w01, uint32_t w10, uint32_t w11, uint32_t& wlo, uint32_t& whi)
+{
+    pack_w8_halves((w00 & 0xffffu) | (w01 << 16), (w10 & 0xffffu) | (w11 << 16), wlo, whi);
+}
 VO_DEV uint32_t pack_w(int w00, int w01, int w10, int w11, int shift, int mask)
 {
     return (uint32_t)((w00 >> shift) & mask) | ((uint32_t)((w01 >> shift) & mask) << 8) |
@@ -1017,13 +1039,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 #endif
                 // row r bytes Wa0..Wa4 = bytes jsh .. jsh + 4 of (a1:a0), row r + 1 likewise Wb: A / C
                 // hold W0..W3, Bv / D hold W1..W4 (byte-select by an SGPR selector, which also
-                // covers jsh + 1 = 4); quad i = (Wa_i, Wa_i+1, Wb_i, Wb_i+1), one permute each
+                // covers jsh + 1 = 4); quad i = (Wa_i, Wb_i, Wa_i+1, Wb_i+1) (the weights' byte
+                // order, pack_w8), one permute each
                 const uint32_t A = __builtin_amdgcn_alignbyte(a1, a0, jsh);
                 const uint32_t Bv = __builtin_amdgcn_perm(a1, a0, jsel1);
                 const uint32_t C = __builtin_amdgcn_alignbyte(b1, b0, jsh);
                 const uint32_t D = __builtin_amdgcn_perm(b1, b0, jsel1);
-                QT4[r * QM + m] = make_uint4(__builtin_amdgcn_perm(C, A, 0x05040100u), __builtin_amdgcn_perm(C, A, 0x06050201u),
-                                             __builtin_amdgcn_perm(C, A, 0x07060302u), __builtin_amdgcn_perm(D, Bv, 0x07060302u));
+                QT4[r * QM + m] = make_uint4(__builtin_amdgcn_perm(C, A, 0x05010400u), __builtin_amdgcn_perm(C, A, 0x06020501u),
+                                             __builtin_amdgcn_perm(C, A, 0x07030602u), __builtin_amdgcn_perm(D, Bv, 0x07030602u));
             }
         }
         wave_lds_sync();
@@ -1061,6 +1084,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
         float ox = 0.f, oy = 0.f;   // nextPts[ptidx]
         for (level = level_hi; level >= level_lo; --level) {
         cols = P.lw[level]; rows = P.lh[level]; pitch = P.lpitch[level]; loff = (int)P.loff[level];
+        const unsigned colsW = (unsigned)(cols + WW), rowsW = (unsigned)(rows + WH);
         const float sc = __builtin_ldexpf(1.f, -level);     // 1 / 2^level, exact (no f64 division)
         float px = ptx * sc, py = pty * sc;
         if (level == P.L) { ox = px; oy = py; }
@@ -1119,6 +1143,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                         LKPROF_ADD(3, 1);
                         j_origin(jx, jy);
                         j_issue(vjr);
+                    } else {
+                        tx0 = ty0 = -(1 << 28);        // no tile: the first iteration's test restages
                     }
                 }
                 wave_lds_sync();
@@ -1227,14 +1253,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     // floor(n) as a float is exact, so n - floor(n) == n - (float)(int)floor(n)
                     const float fnx = floorf(nx), fny = floorf(ny);
                     const int inx = (int)fnx, iny = (int)fny;
-                    if (inx < -WW || inx >= cols || iny < -WH || iny >= rows) {
+                    // inx < -WW || inx >= cols || iny < -WH || iny >= rows, as two unsigned compares
+                    if ((unsigned)(inx + WW) >= colsW || (unsigned)(iny + WH) >= rowsW) {
                         if (level == 0) status = 0;
                         break;
                     }
-                    if (!staged || (unsigned)(inx - tx0) > 2u * LK_M || (unsigned)(iny - ty0) > 2u * LK_M) {
-                        stage_j(inx, iny);
-                        staged = true;
-                    }
+                    // (tx0, ty0 hold a far-away sentinel while no tile is staged at this level)
+                    if ((unsigned)(inx - tx0) > 2u * LK_M || (unsigned)(iny - ty0) > 2u * LK_M) stage_j(inx, iny);
                     a = nx - fnx;
                     bb = ny - fny;
                     // wave-uniform weights: into scalar registers, packed by the scalar unit.
@@ -1251,8 +1276,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                     const int w11 = (int)((1u << 14) + 3u * 0x4B400000u - u00 - u01 - u10);
                     // iw11 can be -1: dot with w11 + 1 and subtract the tap once
                     const int neg = w11 < 0;
-                    const uint32_t wlo = pack_w((int)u00, (int)u01, (int)u10, w11 + neg, 0, 127);
-                    const uint32_t whi = pack_w((int)u00, (int)u01, (int)u10, w11 + neg, 7, 255);
+                    uint32_t wlo, whi;
+                    pack_w8(u00, u01, u10, (uint32_t)(w11 + neg), wlo, whi);
                     const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int b1 = 0, b2 = 0;
                     // all four quads read before the (wave-uniform) branch: one LDS round trip
@@ -1265,7 +1290,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
 #pragma unroll
                         for (int j = 0; j < MAXJ; ++j) {
                             const uint32_t q = qv[j];
-                            uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                            uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 8) +
                                            __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                             if (decltype(negc)::value) sum -= q >> 24;
                             dd[j] = (uint32_t)((int)sum >> 9);       // |diff| <= 8160: an int16
@@ -1330,21 +1355,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                         status = 0;
                         break;
                     }
-                    if (!staged || inx < tx0 || inx > tx0 + 2 * LK_M || iny < ty0 || iny > ty0 + 2 * LK_M) stage_j(inx, iny);
+                    if ((unsigned)(inx - tx0) > 2u * LK_M || (unsigned)(iny - ty0) > 2u * LK_M) stage_j(inx, iny);
                     const float aa = fx - inx, cc = fy - iny;
                     const int w00 = __float2int_rn((1.f - aa) * (1.f - cc) * (float)(1 << 14));
                     const int w01 = __float2int_rn(aa * (1.f - cc) * (float)(1 << 14));
                     const int w10 = __float2int_rn((1.f - aa) * cc * (float)(1 << 14));
                     const int w11 = (1 << 14) - w00 - w01 - w10;
                     const int neg = w11 < 0;
-                    const uint32_t wlo = pack_w(w00, w01, w10, w11 + neg, 0, 127);
-                    const uint32_t whi = pack_w(w00, w01, w10, w11 + neg, 7, 255);
+                    uint32_t wlo, whi;
+                    pack_w8_v((uint32_t)w00, (uint32_t)w01, (uint32_t)w10, (uint32_t)(w11 + neg), wlo, whi);
                     const uint32_t* tb = QT + (iny - ty0) * QS + (inx - tx0);
                     int es = 0;
 #pragma unroll
                     for (int j = 0; j < MAXJ; ++j) {
                         const uint32_t q = tb[toff[j]];
-                        uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 7) +
+                        uint32_t sum = (__builtin_amdgcn_udot4(q, whi, 0u, false) << 8) +
                                        __builtin_amdgcn_udot4(q, wlo, iseed[j], false);
                         if (neg) sum -= q >> 24;
                         const int diff = (int)sum >> 9;
