@@ -1099,7 +1099,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
         py -= hy;
         const int ipx = (int)floorf(px), ipy = (int)floorf(py);
         do {
-            if (ipx < -WW || ipx >= cols || ipy < -WH || ipy >= rows) {
+            if ((unsigned)(ipx + WW) >= colsW || (unsigned)(ipy + WH) >= rowsW) {   // outside the level
                 if (level == 0) { status = 0; errv = 0.f; }
                 break;
             }
@@ -1138,7 +1138,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 }
                 {
                     const int jx = (int)floorf(ox - hx), jy = (int)floorf(oy - hy);
-                    staged = LK_JPRE && !(jx < -WW || jx >= cols || jy < -WH || jy >= rows) && P.max_count > 0;
+                    staged = LK_JPRE && (unsigned)(jx + WW) < colsW && (unsigned)(jy + WH) < rowsW && P.max_count > 0;
                     if (staged) {
                         LKPROF_ADD(3, 1);
                         j_origin(jx, jy);
