@@ -760,11 +760,11 @@ def main():
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes_per_launch": bytes_by[dom], "mean_ms": round(dom_ms, 4)}
 
-    # k_lk_w is VALU-issue bound (profiles/*_sq.txt): achieved VALU wave-instructions/s from the
+    # k_lk_w is issue bound, VALU and the CU's scalar unit together: achieved VALU wave-instructions/s from the
     # profiled instructions per tracked point (profiles/lk_valu.json, rocprofv3 SQ_INSTS_VALU at
     # the same config) x the points of this run / the live track time, against the CDNA4 issue
     # peak (32-wide SIMDs: a wave64 VALU instruction every 2 cycles per SIMD)
-    roof_valu = None
+    roof_valu = roof_salu = None
     vj = os.path.join(ROOT, "profiles", "lk_valu.json")
     if os.path.exists(vj):
         try:
@@ -775,6 +775,15 @@ def main():
             roof_valu = {"bound": "valu", "kernel": "k_lk_w", "achieved": round(ach_vi / 1e9, 2), "peak": peak_vi / 1e9,
                          "unit": "G VALU wave-instr/s", "frac": round(ach_vi / peak_vi, 4),
                          "valu_per_point": round(float(vr["valu_per_point"]), 1), "profile": vr.get("tag")}
+            # the kernel's other issue limit (round 6): a CU has ONE scalar unit for its four
+            # SIMDs, so SALU instructions retire at most once per cycle per CU (256 x 2.4 GHz)
+            if vr.get("salu_insts_per_launch") and vr.get("points_per_launch"):
+                sp = float(vr["salu_insts_per_launch"]) / float(vr["points_per_launch"])
+                peak_si = 256 * 2.4e9
+                ach_si = sp * npts / (dom_ms * 1e-3)
+                roof_salu = {"bound": "salu (one scalar unit per CU)", "kernel": "k_lk_w", "achieved": round(ach_si / 1e9, 2),
+                             "peak": peak_si / 1e9, "unit": "G SALU instr/s", "frac": round(ach_si / peak_si, 4),
+                             "salu_per_point": round(sp, 1), "profile": vr.get("tag")}
         except (OSError, ValueError, KeyError):
             roof_valu = None
 
@@ -798,6 +807,7 @@ def main():
                    "seed": args.seed},
         "roofline": roof,
         "roofline_valu": roof_valu,
+        "roofline_salu": roof_salu,
         "stages_ms": stage,
         "chains_ok": n_ok_all,
         "chains_failed": world * B - n_ok_all,
