@@ -1562,6 +1562,24 @@ __global__ void __launch_bounds__(256) k_eignms(EigParams P)
 VO_DEV int dpp_from_left(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, false); }   // lane i <- i-1
 VO_DEV int dpp_from_right(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, false); }  // lane i <- i+1
 
+// sqrt of a double holding an integer in [0, 2^53): the compiler's correctly rounded sequence
+// (v_rsq_f64 + Newton steps with a final fma correction) without its range reduction for inputs
+// below 2^-767 and its class fix-ups, which such inputs never need; 0 (rsq = inf) selects 0.
+// Bit-identical to sqrt() there, ~5 instructions shorter per pixel in k_eig3.
+VO_DEV double sqrt_int_f64(double x)
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return x == 0.0 ? 0.0 : g;
+}
+
 __global__ void __launch_bounds__(64) k_eig3(EigParams P)
 {
     __shared__ uint64_t kbuf[E3_CAP];
@@ -1610,7 +1628,7 @@ __global__ void __launch_bounds__(64) k_eig3(EigParams P)
         const int sxx = ax + bx + cx, sxy = ay + by + cy, syy = az + bz + cz;
         const int T = sxx + syy, dd = sxx - syy;
         const double Dd = (double)dd * (double)dd + 4.0 * ((double)sxy * (double)sxy);
-        const float v = (float)(((double)T - sqrt(Dd)) * sc);
+        const float v = (float)(((double)T - sqrt_int_f64(Dd)) * sc);
         if (own && r >= y0 && r < m1) {
             const uint32_t k = fkey(v);
             kmax = k > kmax ? k : kmax;
