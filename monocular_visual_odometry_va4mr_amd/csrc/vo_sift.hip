@@ -1038,7 +1038,36 @@ VO_DEV void lds_rmw_add4_lanes(float* p, float v0, float v1, float v2, float v3,
                  "ds_write_b32 %2, %1\n\ts_mov_b64 exec, %0"
                  : "=&s"(save), "=&v"(h)
                  : "v"(a), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(lanes)
-                 : "memory");
+                 : "memory", "scc");        // s_and_b64 writes SCC
+}
+
+// The eight read-add-writes of one group of sub-runs (lanes 8 j .. 8 j + 7 serve sub-run j), in
+// sub-run order, as one asm block: exec is set to the group's lanes by one 32-bit SALU op per
+// step (steps 0-3 in exec_lo, 4-7 in exec_hi) instead of saving / masking / restoring it around
+// every step (k_sift_desc_w shares the CU's one scalar unit with its VALU work; SALU-heavy code
+// waits on it).  Same LDS operations in the same order as eight lds_rmw_add4_lanes calls.
+VO_DEV void lds_rmw_add4_walk8(float* p, float v0, float v1, float v2, float v3, uint64_t am)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)p;
+    const uint32_t am_lo = (uint32_t)am, am_hi = (uint32_t)(am >> 32);
+    uint64_t save;
+    float h;
+#define VO_RMW4 "ds_read_b32 %1, %2\n\ts_waitcnt lgkmcnt(0)\n\tv_add_f32 %1, %1, %3\n\tv_add_f32 %1, %1, %4\n\t" \
+                "v_add_f32 %1, %1, %5\n\tv_add_f32 %1, %1, %6\n\tds_write_b32 %2, %1\n\t"
+    asm volatile("s_mov_b64 %0, exec\n\t"
+                 "s_mov_b32 exec_hi, 0\n\ts_and_b32 exec_lo, %7, 0xff\n\t" VO_RMW4
+                 "s_and_b32 exec_lo, %7, 0xff00\n\t" VO_RMW4
+                 "s_and_b32 exec_lo, %7, 0xff0000\n\t" VO_RMW4
+                 "s_and_b32 exec_lo, %7, 0xff000000\n\t" VO_RMW4
+                 "s_mov_b32 exec_lo, 0\n\ts_and_b32 exec_hi, %8, 0xff\n\t" VO_RMW4
+                 "s_and_b32 exec_hi, %8, 0xff00\n\t" VO_RMW4
+                 "s_and_b32 exec_hi, %8, 0xff0000\n\t" VO_RMW4
+                 "s_and_b32 exec_hi, %8, 0xff000000\n\t" VO_RMW4
+                 "s_mov_b64 exec, %0"
+                 : "=&s"(save), "=&v"(h)
+                 : "v"(a), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(am_lo), "s"(am_hi)
+                 : "memory", "scc");        // s_and_b32 writes SCC
+#undef VO_RMW4
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_sift_desc_w(vo_sift_buf sb)
@@ -1203,19 +1232,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                         const int rr = g + (lane >> 3), k = lane & 7;
                         const bool act = rr < ns;
                         const int koff = (0x4746'3D3C'0B0A'0100ull >> (8 * k)) & 0xFF;   // {0,1,10,11,60,61,70,71}
-                        const int s0 = act ? slist[rr] : 0;
-                        const int e0 = act ? (rr + 1 < ns ? slist[rr + 1] : take) : 0;
-                        const int m = e0 - s0;                                           // 1..4
-                        const int addr = act ? pidx[s0] + koff : 0;
+                        // every read unconditional and in bounds (sub-run index clamped, s0 + 3 <= 66
+                        // < the 72-float row), then selects: no exec-mask dance per conditional
+                        // read.  Inactive lanes' values are never used (the walk masks them out);
+                        // an active lane's missing pixels are exact +0 by the selects.
+                        const int rrc = act ? rr : 0;
+                        const int s0 = slist[rrc];
+                        const int s1 = slist[min(rrc + 1, 63)];
+                        const int e0 = rrc + 1 < ns ? s1 : take;
+                        const int m = e0 - s0;                                           // 1..4 if active
+                        const int addr = pidx[s0] + koff;
                         const float* pv = pval + k * 72 + s0;
-                        const float v0 = act ? pv[0] : 0.f;
-                        const float v1 = act && m > 1 ? pv[1] : 0.f;
-                        const float v2 = act && m > 2 ? pv[2] : 0.f;
-                        const float v3 = act && m > 3 ? pv[3] : 0.f;
+                        const float p0 = pv[0], p1 = pv[1], p2 = pv[2], p3 = pv[3];
+                        const float v0 = p0;
+                        const float v1 = m > 1 ? p1 : 0.f;
+                        const float v2 = m > 2 ? p2 : 0.f;
+                        const float v3 = m > 3 ? p3 : 0.f;
                         const uint64_t am = __ballot(act);
-        #pragma unroll
-                        for (int j = 0; j < 8; ++j)
-                            lds_rmw_add4_lanes(hist + addr, v0, v1, v2, v3, am & (0xFFull << (8 * j)));
+                        lds_rmw_add4_walk8(hist + addr, v0, v1, v2, v3, am);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
