@@ -600,14 +600,6 @@ VO_DEV bool lk_block(int B, int nb, int& b, int& pb, bool xcd = true, int L = -1
 // over the 14-bit weights split into 7+7 bits; all window sums are integer and exact, so
 // results match the CPU restatement bit for bit.
 #define LK_M 4
-// a zero the compiler cannot see through: per-lane index math that uses it is recomputed at
-// each staging instead of being hoisted out of the point / level loops into live VGPRs
-VO_DEV int opaque0()
-{
-    int z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    return z;
-}
 // buffer resource over one chain's buffer: loads take 32-bit offsets (one VGPR, not a 64-bit
 // address) and read zeros outside [0, bytes) instead of faulting
 VO_DEV __amdgpu_buffer_rsrc_t lkq_rsrc(const void* base, int64_t bytes)
@@ -1004,7 +996,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     // the dword to the right from the neighbouring lane (DPP) and row r + 1 from its own b load
     auto j_issue = [&](uint32_t (&v)[2][NJR]) {
         const int gx0 = tx0 + VO_BORDER, gy0 = ty0 + VO_BORDER;
-        const int ln = lane + opaque0();
+        const int ln = lane;
         const int vo = loff + gy0 * pitch + (gx0 & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);
 #pragma unroll
         for (int k = 0; k < NJR; ++k) {
@@ -1023,7 +1015,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
     // and two rounds of byte permutes, stored as one 16-B write; quad byte order (J[r][c],
     // J[r][c+1], J[r+1][c], J[r+1][c+1])
     auto j_store = [&](const uint32_t (&v)[2][NJR]) {
-        const int ln = lane + opaque0();
+        const int ln = lane;
         const int m = ln & 7;
         const uint32_t jsel1 = (uint32_t)(jsh + 1) * 0x01010101u + 0x03020100u;   // bytes jsh+1 .. jsh+4
 #pragma unroll
@@ -1110,7 +1102,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 LKPROF_T(ti0);
                 const int gx = ipx + VO_BORDER, gy = ipy + VO_BORDER;
                 const int ish = gx & 3;
-                const int ln = lane + opaque0();
+                const int ln = lane;
                 const int vi = loff + gy * pitch + (gx & ~3) + (ln >> 3) * pitch + 4 * (ln & 7);   // 8 dwords / row
                 // 16 (dx, dy) per row; lane -> row 4k + 2 ((ln >> 4) & 1) + (ln >> 5): the two rows a
                 // 32-lane half stores are 2 apart (2 QS = 48 dwords, 16 banks), so the ds_write_b32
