@@ -54,22 +54,24 @@ VO_DEV float exp32f(float x, const float* tab)
     return two * tab[xi & 63] * ((((x0 + A1) * x0 + A2) * x0 + A3) * x0 + A4);
 }
 
+// a wave-uniform float (every lane holds the same value) in a scalar register
+VO_DEV float uniform_f(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+
 VO_DEV float fast_atan2(float y, float x)
 {
     const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
     const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
     const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
     const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
-    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    // OpenCV's two branches (|x| >= |y|: c = |y| / (|x| + eps), a = poly(c); else c = |x| / (|y| +
+    // eps), a = 90 - poly(c)) as one division and one polynomial on selected operands: the same
+    // operations per lane, but a wave whose lanes take both branches no longer runs both
+    const float ax = fabsf(x), ay = fabsf(y);
+    const bool xge = ax >= ay;
+    const float c = (xge ? ay : ax) / ((xge ? ax : ay) + (float)DBL_EPSILON);
+    const float c2 = c * c;
+    const float pc = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    float a = xge ? pc : 90.f - pc;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;
@@ -160,6 +162,7 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
     float* s_row = s_dyn + (BT_H + 2 * r) * sst;
     const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
     src += blockIdx.z * src_stride;
+    const bool wdst = dst != nullptr;                  // null: the DoG alone (top layer)
     dst += blockIdx.z * dst_stride;
     if (tid < n) s_k[tid] = kern[tid];
     const int rows = BT_H + 2 * r, cols = BT_W + 2 * r;
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(256) k_blur_tile(const float* __restrict__ src
             for (int j = 0; j < 4; ++j) {
                 const int gy = y0 + tyh + j;
                 if (gy >= h || gx >= w) continue;
-                dst[(int64_t)gy * w + gx] = acc[j];
+                if (wdst) dst[(int64_t)gy * w + gx] = acc[j];
                 if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx] = acc[j] - s_src[(tyh + j + r) * sst + tx + r];
             }
         }
@@ -258,6 +261,7 @@ __global__ void __launch_bounds__(256) k_blur_tile_n(const float* __restrict__ s
     const int tid = threadIdx.x;
     const int x0 = blockIdx.x * BT_W, y0 = blockIdx.y * BT_H;
     src += blockIdx.z * src_stride;
+    const bool wdst = dst != nullptr;                  // null: the DoG alone (top layer)
     dst += blockIdx.z * dst_stride;
     float kk[N];
 #pragma unroll
@@ -328,7 +332,7 @@ __global__ void __launch_bounds__(256) k_blur_tile_n(const float* __restrict__ s
             for (int e = 0; e < 2; ++e) {
                 if (gx + e >= w) continue;
                 const float o = e ? a[j].y : a[j].x;
-                dst[(int64_t)gy * w + gx + e] = o;
+                if (wdst) dst[(int64_t)gy * w + gx + e] = o;
                 if (dog) dog[blockIdx.z * dog_stride + (int64_t)gy * w + gx + e] = o - cs[e];
             }
         }
@@ -637,6 +641,7 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
         const int n = SIFT_ORI_HIST_BINS;
         const float expf_scale = -1.f / (2.f * sigma * sigma);
         const int side = 2 * radius + 1, total = side * side;
+        const float inv_side = 1.f / (float)side;
         float th = 0.f;                                   // temphist[lane] for lane < 36
         for (int base = 0; base < total; base += 64) {
             const int pos = base + lane;
@@ -644,7 +649,8 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
             int bin = 0;
             float val = 0.f;
             if (pos < total) {
-                const int ii = pos / side;
+                // pos / side from the float reciprocal: exact (pos < 2^20; margin 0.5 / side)
+                const int ii = (int)(((float)pos + 0.5f) * inv_side);
                 const int i = ii - radius, j = pos - ii * side - radius;
                 const int y = py + i, x = px + j;
                 valid = y > 0 && y < ht - 1 && x > 0 && x < wd - 1;
@@ -1111,17 +1117,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         uint32_t* ring = ring_s[w];
         int* slist = slist_s[w];
         const float* tab = tab_s;
+        // the keypoint's fields are wave-uniform: read them into scalar registers, so that every
+        // quantity derived from them (window radius, trip counts, ring state) is known uniform and
+        // the loops below branch on scalars instead of exec masks
         const float* kp = im.kp_out + 6 * (int64_t)q;
-        const int kpo = (int)kp[5];
+        const int kpo = __builtin_amdgcn_readfirstlane((int)kp[5]);
         int octave = kpo & 255, layer = (kpo >> 8) & 255;
         octave = octave < 128 ? octave : (-128 | octave);
         const float scale = octave >= 0 ? 1.f / (1 << octave) : (float)(1 << -octave);
-        const float size = kp[2] * scale;
-        const float ptx = kp[0] * scale, pty = kp[1] * scale;
+        const float size = uniform_f(kp[2]) * scale;
+        const float ptx = uniform_f(kp[0]) * scale, pty = uniform_f(kp[1]) * scale;
         const int oi = octave + 1;
         const float* img = im.gauss + sb.gauss_off[oi * (N_LAYERS + 3) + layer];
         const int cols = sb.oct_w[oi], rows = sb.oct_h[oi];
-        float angle = 360.f - kp[3];
+        float angle = 360.f - uniform_f(kp[3]);
         if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
         const float ori = angle, scl = size * 0.5f;
         const int d = 4, n = 8;
@@ -1161,8 +1170,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             const float rbin = r_rot + d / 2 - 0.5f;
             const float cbin = c_rot + d / 2 - 0.5f;
             const int r = ptiy + i, c = ptix + j;
-            const bool valid = pos < total && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < rows - 1 &&
-                               c > 0 && c < cols - 1;
+            // every term evaluated (no short circuit: one flat mask computation, no exec juggling)
+            const bool valid = (pos < total) & (rbin > -1) & (rbin < d) & (cbin > -1) & (cbin < d) & (r > 0) &
+                               (r < rows - 1) & (c > 0) & (c < cols - 1);
             const uint64_t m = __ballot(valid);
             if (valid)
                 ring[(head + pend + __popcll(m & ((1ull << lane) - 1ull))) & 127] =
@@ -1271,23 +1281,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the two norms: every square is formed per lane (the same rounded products), only the
+        // 128 additions stay sequential on lane 0, in the serial order
         const int len = d * d * n;
+        float* sq = pval_s[w] + 128;
+        for (int t = lane; t < len; t += 64) sq[t] = dsl[t] * dsl[t];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane == 0) {
             float nrm2 = 0;
-            for (int k = 0; k < len; ++k) nrm2 += dsl[k] * dsl[k];
-            const float thr = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
-            nrm2 = 0;
-            for (int i = 0; i < len; ++i) {
-                const float v = dsl[i] < thr ? dsl[i] : thr;
-                nrm2 += v * v;
-            }
-            red_s[w][0] = thr;
-            red_s[w][1] = nrm2;
+            for (int k = 0; k < len; ++k) nrm2 += sq[k];
+            red_s[w][0] = sqrtf(nrm2) * SIFT_DESCR_MAG_THR;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const float thr = red_s[w][0];
+        for (int t = lane; t < len; t += 64) {
+            const float v = dsl[t] < thr ? dsl[t] : thr;
+            sq[t] = v * v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {
+            float nrm2 = 0;
+            for (int k = 0; k < len; ++k) nrm2 += sq[k];
+            red_s[w][1] = nrm2;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const float s2 = sqrtf(red_s[w][1]);
         const float nscale = SIFT_INT_DESCR_FCTR / (s2 > FLT_EPSILON ? s2 : FLT_EPSILON);
         float* dst = im.desc + 128 * (int64_t)q;
@@ -1460,9 +1485,12 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
             hipLaunchKernelGGL(k_nn_down, dim3((w + 127) / 128, h, nb), dim3(128), 0, st, src, sb->oct_w[o - 1],
                                sb->oct_h[o - 1], sb->gauss + sb->gauss_off[o * 6], w, h, gs);
         }
-        // G_i = blur(G_{i-1}); the same pass writes D_{i-1} = G_i - G_{i-1}
+        // G_i = blur(G_{i-1}); the same pass writes D_{i-1} = G_i - G_{i-1}.  The top layer
+        // G_{N_LAYERS+2} is only ever read through its DoG (keypoints live on layers 1..N_LAYERS,
+        // the next octave starts from G_{N_LAYERS}), so that pass writes the DoG alone
         for (int i = 1; i < N_LAYERS + 3; ++i)
-            blur(sb->gauss + sb->gauss_off[o * 6 + i - 1], gs, sb->gauss + sb->gauss_off[o * 6 + i],
+            blur(sb->gauss + sb->gauss_off[o * 6 + i - 1], gs,
+                 i < N_LAYERS + 2 ? sb->gauss + sb->gauss_off[o * 6 + i] : nullptr,
                  sb->dog + sb->dog_off[o * 5 + i - 1], w, h, i);
     }
     for (int o = 0; o < sb->n_oct; ++o) {
