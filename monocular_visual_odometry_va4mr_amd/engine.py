@@ -468,7 +468,23 @@ class Engine:
             self._sift = None
             torch.cuda.empty_cache()
             self._sift = Sift(self.W, self.H, self.device, batch=2 * m, nfeatures=nfeat)
+            self._load_bootstrap_glue()
         return self._sift, m
+
+    def _load_bootstrap_glue(self):
+        """Run the bootstrap's few torch-side glue ops (strided counter reads, the capacity-flag
+        merge, the status select) once on the fresh workspace's zeroed counters, so that their
+        GPU code is loaded here, with the workspace, and not in the first bootstrap: HIP loads a
+        kernel's code object at its first launch, and one such load inside the first bootstrap
+        blocked the host for 0.1 s (GPU idle up to 44 ms, tools/boot_api_trace.sh).  Writes
+        nothing the bootstrap reads (the results are discarded)."""
+        c = self._sift.t["counters"][:2]
+        f = c[:, 3]
+        ovf = torch.zeros(1, dtype=torch.int32, device=self.device)
+        ovf[0:1] = torch.maximum(f[:1], f[1:])
+        n = c[:, 2].contiguous()
+        ovf[0:1] = n[:1]
+        torch.where(ovf > 0, torch.full_like(ovf, L.ST_CAPACITY), ovf)
 
     def release_bootstrap(self):
         """Free the SIFT workspace and the matcher scratch (stepping never needs them)."""
