@@ -569,8 +569,12 @@ class Headline:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if reserve:
-            for e in self.engines:
-                e.reserve_bootstrap()                 # SIFT workspace (the reference's SIFT_create)
+            # SIFT workspace (the reference's SIFT_create), each on the stream its engine
+            # bootstraps on: the workspace's first kernels also bring up that stream (a HIP stream
+            # of torch's pool is created at its first use, ~6 ms, which the first bootstrap paid)
+            for g, e in enumerate(self.engines):
+                with torch.cuda.stream(self.streams[g]):
+                    e.reserve_bootstrap()
         torch.cuda.synchronize()
         self.boot_alloc_s = time.perf_counter() - t0
 

@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(128) k_sift_refine(vo_sift_buf sb)
 __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
 {
     const SiftImg im = sift_img(sb, blockIdx.z);
-    __shared__ int4 pb_s4[4][16];
+    __shared__ int4 pb_s4[4][18];
     __shared__ float4 pv_s4[4][16];
     __shared__ float th_s[4][SIFT_ORI_HIST_BINS + 4];
     __shared__ float hs_s[4][SIFT_ORI_HIST_BINS];
@@ -626,12 +626,17 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
     const int rec_cap = (int)(((int64_t)sb.kp_cap * 360) / SIFT_REC);
     const int n_rec = min(im.counters[4], rec_cap);
     for (int q = blockIdx.x * 4 + w; q < n_rec; q += gridDim.x * 4) {   // wave-uniform loop
-        int* pbin = reinterpret_cast<int*>(pb_s4[w]);
-        float* pval = reinterpret_cast<float*>(pv_s4[w]);
+        int* pcnt = reinterpret_cast<int*>(pb_s4[w]);      // per bin: its pixels in the chunk
+        int* poff = pcnt + 36;                              // per bin: its first slot
+        float* pval = reinterpret_cast<float*>(pv_s4[w]);  // the chunk's values sorted by bin
         const float* rec = im.hist + (int64_t)SIFT_REC * q;
-        const float kx = rec[0], ky = rec[1], ksize = rec[2], kresp = rec[3];
-        const int koct = __float_as_int(rec[4]), o = __float_as_int(rec[5]), layer = __float_as_int(rec[6]);
-        const int py = __float_as_int(rec[7]), px = __float_as_int(rec[8]);
+        // wave-uniform record fields in scalar registers (scalar loop control below)
+        const float kx = rec[0], ky = rec[1], ksize = uniform_f(rec[2]), kresp = rec[3];
+        const int koct = __float_as_int(rec[4]);
+        const int o = __builtin_amdgcn_readfirstlane(__float_as_int(rec[5]));
+        const int layer = __builtin_amdgcn_readfirstlane(__float_as_int(rec[6]));
+        const int py = __builtin_amdgcn_readfirstlane(__float_as_int(rec[7]));
+        const int px = __builtin_amdgcn_readfirstlane(__float_as_int(rec[8]));
         const float* tab = sb.consts + EXPTAB_OFF;
         const float scl_octv = ksize * 0.5f / (float)(1 << o);
         const float* img = im.gauss + sb.gauss_off[o * (N_LAYERS + 3) + layer];
@@ -666,29 +671,50 @@ __global__ void __launch_bounds__(256) k_sift_ori(vo_sift_buf sb)
                     val = wt * mag;
                 }
             }
+            // Each bin's pixels must reach th in lane (= the serial raster) order.  The chunk's
+            // valid pixels are sorted by bin, stably: a pixel's slot is the start of its bin
+            // (an exclusive scan of the per-bin counts) plus its rank among the pixels of its bin
+            // in lower lanes.  `eq` = the lanes holding my bin, from six bit-sliced ballots of the
+            // 6-bit bin (invalid lanes hold bin 0 and are masked out by `m`).  Lane b then adds
+            // its bin's pixels slot by slot: the same additions, in the same order, as the
+            // pixel-by-pixel walk, in max-per-bin rounds instead of one pass per four pixels.
             const uint64_t m = __ballot(valid);
-            const int nv = __popcll(m);
-            if (valid) {
-                const int slot = __popcll(m & ((1ull << lane) - 1ull));
-                pbin[slot] = bin;
-                pval[slot] = val;
+            uint32_t eq_lo = (uint32_t)m, eq_hi = (uint32_t)(m >> 32);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const uint32_t mine = (uint32_t)(-((bin >> k) & 1));      // ~0 if my bit k is set
+                const uint64_t bk = __ballot(mine != 0u);
+                eq_lo &= ~((uint32_t)bk ^ mine);
+                eq_hi &= ~((uint32_t)(bk >> 32) ^ mine);
             }
-            // slots nv .. (nv rounded up to 4) get bin -1, which no lane owns: the walk below
-            // needs no bounds test per pixel
-            if (lane >= nv && lane < ((nv + 3) & ~3)) pbin[lane] = -1;
+            const int rank = (int)__builtin_amdgcn_mbcnt_hi(eq_hi, __builtin_amdgcn_mbcnt_lo(eq_lo, 0u));
+            const int cnt_p = __popc(eq_lo) + __popc(eq_hi);
+            if (lane < n) pcnt[lane] = 0;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // four pixels per step; a pixel of another bin adds +0, which leaves th unchanged
-            // (th and every value are >= +0)
-            for (int p0 = 0; p0 < nv; p0 += 4) {
-                const int4 bb = *reinterpret_cast<const int4*>(pbin + p0);
-                const float4 vv = *reinterpret_cast<const float4*>(pval + p0);
-                th += bb.x == lane ? vv.x : 0.f;
-                th += bb.y == lane ? vv.y : 0.f;
-                th += bb.z == lane ? vv.z : 0.f;
-                th += bb.w == lane ? vv.w : 0.f;
+            if (valid) pcnt[bin] = cnt_p;                   // every pixel of a bin writes the same
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int c = lane < n ? pcnt[lane] : 0;        // pixels of bin `lane`
+            int incl = c;                                   // inclusive scan over the lanes
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += y;
             }
+            const int off = incl - c;                       // first slot of bin `lane`
+            if (lane < n) poff[lane] = off;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid) pval[poff[bin] + rank] = val;        // slots 0 .. popc(m) - 1
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int k = 0; __ballot(k < c) != 0ull; ++k)
+                if (k < c) th += pval[off + k];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

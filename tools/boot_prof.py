@@ -28,8 +28,9 @@ engines = [Engine(rend.K, opts, rend.W, rend.H, batch=bounds[g + 1] - bounds[g],
 streams = [torch.cuda.Stream(dev) for _ in range(G)]
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-for e in engines:
-    e.reserve_bootstrap()
+for g, e in enumerate(engines):
+    with torch.cuda.stream(streams[g]):           # as bench.py: brings up the group's stream too
+        e.reserve_bootstrap()
 torch.cuda.synchronize()
 print(f"workspace {time.perf_counter() - t0:.3f} s", flush=True)
 for rep in range(3):
