@@ -108,31 +108,39 @@ VO_DEV SiftImg sift_img(const vo_sift_buf& sb, int z)
 }
 
 // ------------------------------------------------------- scale space
-__global__ void k_upsample(const uint8_t* __restrict__ img, int64_t img_stride, int w, int h, float* __restrict__ dst,
-                           int64_t dst_stride)
+// 2x bilinear upsample (INTER_LINEAR, the reference's resize of the base image).  A block covers
+// UP_ROWS output rows; a thread, one column of them (a one-row, 128-thread block per output row
+// made 5.8 M blocks per 384-image launch, bound by block dispatch rather than by its 3 GB of
+// stores).  The per-pixel arithmetic is unchanged.
+#define UP_ROWS 8
+__global__ void __launch_bounds__(256) k_upsample(const uint8_t* __restrict__ img, int64_t img_stride, int w, int h,
+                                                  float* __restrict__ dst, int64_t dst_stride)
 {
-    const int dx = blockIdx.x * blockDim.x + threadIdx.x, dy = blockIdx.y;
-    const int dw = 2 * w;
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dw = 2 * w, dh = 2 * h;
     if (dx >= dw) return;
     img += blockIdx.z * img_stride;
     dst += blockIdx.z * dst_stride;
-    float fy = (float)((dy + 0.5) * 0.5 - 0.5);
-    int sy = (int)floorf(fy);
-    fy -= sy;
-    if (sy < 0) { fy = 0; sy = 0; }
-    if (sy >= h - 1) { fy = 0; sy = h - 1; }
-    const int sy1 = sy + 1 < h ? sy + 1 : h - 1;
     float fx = (float)((dx + 0.5) * 0.5 - 0.5);
     int sx = (int)floorf(fx);
     fx -= sx;
     if (sx < 0) { fx = 0; sx = 0; }
     if (sx >= w - 1) { fx = 0; sx = w - 1; }
     const int sx1 = sx + 1 < w ? sx + 1 : w - 1;
-    const uint8_t* r0 = img + (int64_t)sy * w;
-    const uint8_t* r1 = img + (int64_t)sy1 * w;
-    const float v0 = (float)r0[sx] * (1.f - fx) + (float)r0[sx1] * fx;
-    const float v1 = (float)r1[sx] * (1.f - fx) + (float)r1[sx1] * fx;
-    dst[(int64_t)dy * dw + dx] = v0 * (1.f - fy) + v1 * fy;
+    const int dy0 = blockIdx.y * UP_ROWS;
+    for (int dy = dy0; dy < dy0 + UP_ROWS && dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * 0.5 - 0.5);
+        int sy = (int)floorf(fy);
+        fy -= sy;
+        if (sy < 0) { fy = 0; sy = 0; }
+        if (sy >= h - 1) { fy = 0; sy = h - 1; }
+        const int sy1 = sy + 1 < h ? sy + 1 : h - 1;
+        const uint8_t* r0 = img + (int64_t)sy * w;
+        const uint8_t* r1 = img + (int64_t)sy1 * w;
+        const float v0 = (float)r0[sx] * (1.f - fx) + (float)r0[sx1] * fx;
+        const float v1 = (float)r1[sx] * (1.f - fx) + (float)r1[sx1] * fx;
+        dst[(int64_t)dy * dw + dx] = v0 * (1.f - fy) + v1 * fy;
+    }
 }
 
 // Separable Gaussian (BORDER_REFLECT_101) of one 64 x 32 output tile per block, both
@@ -1482,7 +1490,8 @@ extern "C" int vo_sift_batch(const vo_sift_buf* sb, int B, const uint8_t* imgs, 
     const unsigned nb = (unsigned)B;
     const int64_t gs = sb->gauss_floats, ds = sb->dog_floats;
     // base: 2x upsample (into the blur scratch) + blur to sigma
-    hipLaunchKernelGGL(k_upsample, dim3((2 * W + 127) / 128, 2 * H, nb), dim3(128), 0, st, imgs, img_stride, W, H,
+    hipLaunchKernelGGL(k_upsample, dim3((2 * W + 255) / 256, (2 * H + UP_ROWS - 1) / UP_ROWS, nb), dim3(256), 0, st, imgs,
+                       img_stride, W, H,
                        sb->tmp, sb->tmp_floats);
     auto blur = [&](const float* src, int64_t src_stride, float* dst, float* dog, int w, int h, int layer) {
         dim3 g((w + BT_W - 1) / BT_W, (h + BT_H - 1) / BT_H, nb);
