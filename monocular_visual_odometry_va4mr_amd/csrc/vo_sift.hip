@@ -386,32 +386,39 @@ __global__ void __launch_bounds__(256) k_extrema_t(vo_sift_buf sb, int o)
     if (tid == 0) s_n = 0;
     const float* dog0 = im.dog + sb.dog_off[o * (N_LAYERS + 2)];
     const int64_t plane = (int64_t)w * h;               // the octave's DoG layers are contiguous
-    // every load of the tile in flight before the first LDS store (fixed, unrolled trip count;
-    // clamped addresses, zeros written outside the octave)
-    constexpr int NT = (N_LAYERS + 2) * (EX_H + 2) * (EX_W + 2), NL = (NT + 255) / 256;
+    // every load of the tile in flight before the first LDS store (fixed, unrolled trip counts;
+    // clamped addresses, zeros written outside the octave).  By rows: the four waves take rows
+    // wy, wy + 4, ... of every layer, the 64 lanes columns 0..63 and lanes 0, 1 columns 64, 65 --
+    // row / column arithmetic only (a flat element index cost two divisions per element)
+    constexpr int TR = EX_H + 2, TC = EX_W + 2, NJ = (TR + 3) / 4;
+    static_assert(TC == 66, "k_extrema_t staging: 64 + 2 columns");
     const __amdgpu_buffer_rsrc_t rdog =
         __builtin_amdgcn_make_buffer_rsrc((void*)dog0, (short)0, (int)(4 * (N_LAYERS + 2) * plane), 0x00020000);
-    float v[NL];
+    const int lx = tid & 63, wy = tid >> 6;
+    const int gx0 = min(x0 - 1 + lx, w - 1), gx1 = min(x0 - 1 + 64 + (lx & 1), w - 1);
+    float v0[N_LAYERS + 2][NJ], v1[N_LAYERS + 2][NJ];
 #pragma unroll
-    for (int k = 0; k < NL; ++k) {
-        const int i = min(tid + 256 * k, NT - 1);
-        const int l = i / ((EX_H + 2) * (EX_W + 2));
-        const int rem = i - l * (EX_H + 2) * (EX_W + 2);
-        const int ty = rem / (EX_W + 2), tx = rem - ty * (EX_W + 2);
-        const int gy = min(y0 - 1 + ty, h - 1), gx = min(x0 - 1 + tx, w - 1);
-        // buffer loads: 32-bit offsets, one VGPR per load
-        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdog, 4 * (l * (int)plane + gy * w + gx), 0, 0));
-    }
+    for (int l = 0; l < N_LAYERS + 2; ++l)
 #pragma unroll
-    for (int k = 0; k < NL; ++k) {
-        const int i = tid + 256 * k;
-        if (i < NT) {
-            const int l = i / ((EX_H + 2) * (EX_W + 2));
-            const int rem = i - l * (EX_H + 2) * (EX_W + 2);
-            const int ty = rem / (EX_W + 2), tx = rem - ty * (EX_W + 2);
-            t[l][ty][tx] = (y0 - 1 + ty < h && x0 - 1 + tx < w) ? v[k] : 0.f;
+        for (int j = 0; j < NJ; ++j) {
+            const int ty = min(wy + 4 * j, TR - 1);
+            const int row = l * (int)plane + min(y0 - 1 + ty, h - 1) * w;
+            // buffer loads: 32-bit offsets, one VGPR per load
+            v0[l][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdog, 4 * (row + gx0), 0, 0));
+            v1[l][j] = lx < 2 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdog, 4 * (row + gx1), 0, 0))
+                              : 0.f;
         }
-    }
+#pragma unroll
+    for (int l = 0; l < N_LAYERS + 2; ++l)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int ty = wy + 4 * j;
+            if (ty < TR) {
+                const bool rin = y0 - 1 + ty < h;
+                t[l][ty][lx] = (rin && x0 - 1 + lx < w) ? v0[l][j] : 0.f;
+                if (lx < 2) t[l][ty][64 + lx] = (rin && x0 - 1 + 64 + lx < w) ? v1[l][j] : 0.f;
+            }
+        }
     __syncthreads();
     const float threshold = (float)floor(0.5 * 0.04 / N_LAYERS * 255 * 1);
     const int tx = tid & (EX_W - 1), ty0 = (tid >> 6) * (EX_H / 4);
